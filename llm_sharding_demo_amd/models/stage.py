@@ -1,0 +1,117 @@
+"""One pipeline stage of a GPT-2 or Llama model.
+
+Generalises the reference's two hard-wired shards (`server.py:51-105`):
+  * ShardA (`server.py:68-86`): wte + wpe + blocks[0:split]   -> stage 0
+  * ShardB (`server.py:90-103`): blocks[split:] + ln_f + lm_head -> stage P-1
+to P stages with an arbitrary layer range each.  Differences by design:
+  * a stage materialises only its own layers (quirk Q4),
+  * the causal mask is explicit in the attention op (quirk Q3),
+  * K/V are appended to the shard-local cache, so decode processes one token
+    per sequence (quirk Q5),
+  * the last stage computes lm_head for the last position of each sequence
+    only (quirk Q6) unless `all_logits` is requested (compat /forward_b).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from ..config import ModelConfig
+from ..ops import Residual, get_backend
+from ..runtime.batch import BatchMeta
+from ..runtime.kv_cache import KVCache
+from .weights import maybe_load
+
+
+class StageModel:
+    def __init__(self, cfg: ModelConfig, layer_start: int, layer_end: int, first: bool,
+                 last: bool, device="cpu", dtype: Optional[torch.dtype] = None, seed: int = 0,
+                 weights_path: Optional[str] = None, max_slots: int = 8, max_seq: int = 1024,
+                 weights: Optional[Dict[str, torch.Tensor]] = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if dtype is None:
+            dtype = torch.float32 if self.device.type == "cpu" else torch.bfloat16
+        self.dtype = dtype
+        self.layer_start, self.layer_end = layer_start, layer_end
+        self.first, self.last = first, last
+        self.layers = range(layer_start, layer_end)
+        if weights is None:
+            weights = maybe_load(cfg, weights_path, self.layers, first, last, seed, self.device, dtype)
+        else:
+            weights = {k: v.to(device=self.device, dtype=dtype).contiguous() for k, v in weights.items()}
+        self.w = weights
+        self.max_seq = min(max_seq, cfg.max_positions)
+        self.kv = KVCache(len(self.layers), max_slots, cfg.n_kv_heads, self.max_seq,
+                          cfg.head_dim, dtype, self.device)
+        self.backend = get_backend(self.device)
+        self.backend.prepare_stage(self)
+
+    # ------------------------------------------------------------------
+    def _lw(self, i: int, name: str) -> torch.Tensor:
+        p = "h." if self.cfg.arch == "gpt2" else "layers."
+        return self.w[f"{p}{i}.{name}"]
+
+    def _gpt2_layer(self, li: int, i: int, r: Residual, meta: BatchMeta) -> None:
+        be, c, w = self.backend, self.cfg, self._lw
+        xn = be.layernorm(r, w(i, "ln_1.weight"), w(i, "ln_1.bias"), c.norm_eps)
+        q = be.qkv_kv_append(xn, w(i, "attn.c_attn.weight"), w(i, "attn.c_attn.bias"),
+                             self.kv.k(li), self.kv.v(li), meta, c)
+        o = be.attention(q, self.kv.k(li), self.kv.v(li), meta)
+        be.linear_residual(o, w(i, "attn.c_proj.weight"), w(i, "attn.c_proj.bias"), r)
+        xn = be.layernorm(r, w(i, "ln_2.weight"), w(i, "ln_2.bias"), c.norm_eps)
+        h = be.linear(xn, w(i, "mlp.c_fc.weight"), w(i, "mlp.c_fc.bias"), act="gelu")
+        be.linear_residual(h, w(i, "mlp.c_proj.weight"), w(i, "mlp.c_proj.bias"), r)
+
+    def _llama_layer(self, li: int, i: int, r: Residual, meta: BatchMeta) -> None:
+        be, c, w = self.backend, self.cfg, self._lw
+        xn = be.rmsnorm(r, w(i, "input_layernorm.weight"), c.norm_eps)
+        q = be.qkv_kv_append(xn, w(i, "self_attn.qkv.weight"), None,
+                             self.kv.k(li), self.kv.v(li), meta, c)
+        o = be.attention(q, self.kv.k(li), self.kv.v(li), meta)
+        be.linear_residual(o, w(i, "self_attn.o_proj.weight"), None, r)
+        xn = be.rmsnorm(r, w(i, "post_attention_layernorm.weight"), c.norm_eps)
+        h = be.linear(xn, w(i, "mlp.gate_up.weight"), None, act="silu_mul")
+        be.linear_residual(h, w(i, "mlp.down_proj.weight"), None, r)
+
+    # ------------------------------------------------------------------
+    def embed(self, ids: torch.Tensor, meta: BatchMeta) -> torch.Tensor:
+        if self.cfg.arch == "gpt2":
+            return self.backend.embed(ids, meta.token_pos, self.w["wte"], self.w["wpe"])
+        return self.backend.embed(ids, meta.token_pos, self.w["embed_tokens"], None)
+
+    def forward(self, meta: BatchMeta, inp: torch.Tensor, all_logits: bool = False) -> torch.Tensor:
+        """inp: token ids int32 [T] (first stage) or hidden fp32 [T, H].
+
+        Returns hidden fp32 [T, H] (non-last stage) or fp32 logits
+        [B, vocab_padded] for the last query of each sequence (last stage;
+        [T, vocab_padded] with all_logits)."""
+        x = self.embed(inp, meta) if self.first else inp
+        r = Residual(x)
+        layer_fn = self._gpt2_layer if self.cfg.arch == "gpt2" else self._llama_layer
+        for li, i in enumerate(self.layers):
+            layer_fn(li, i, r, meta)
+        x = self.backend.flush(r)
+        if not self.last:
+            return x
+        return self.head(x, meta, all_logits)
+
+    def head(self, x: torch.Tensor, meta: BatchMeta, all_logits: bool = False) -> torch.Tensor:
+        be, c = self.backend, self.cfg
+        if not all_logits and not meta.is_decode:
+            x = be.gather_rows(x, meta.last_idx)
+        if c.arch == "gpt2":
+            xn = be.norm_rows(x, self.w["ln_f.weight"], self.w["ln_f.bias"], c.norm_eps, rms=False)
+            return be.logits(xn, self.lm_head_weight)
+        xn = be.norm_rows(x, self.w["norm.weight"], None, c.norm_eps, rms=True)
+        return be.logits(xn, self.lm_head_weight)
+
+    @property
+    def lm_head_weight(self) -> torch.Tensor:
+        if hasattr(self, "_lm_head_padded"):
+            return self._lm_head_padded
+        return self.w["wte"] if self.cfg.arch == "gpt2" else self.w["lm_head"]
+
+    def weight_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.w.values())

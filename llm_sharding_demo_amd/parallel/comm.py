@@ -1,0 +1,290 @@
+"""Inter-stage transports.
+
+Reference transport (`server.py:171-181`): per decode step the coordinator
+POSTs all token ids to shard A, receives the hidden states as nested JSON
+lists, re-POSTs them to shard B and receives [1, S, 50257] fp32 logits as
+JSON (8-68 MB per step).  Hidden states are relayed through
+the coordinator; A and B never talk directly.
+
+Here stage i sends its boundary hidden state straight to stage i+1 and the
+last stage sends the sampled token ids (int32 [B]) back to stage 0:
+
+* `NcclTransport` -- torch.distributed over RCCL (backend "nccl" on ROCm),
+  one process per MI355X.  Every pipeline edge i->i+1 and the token-return
+  edge P-1->0 gets its OWN communicator (its own process group), so each
+  edge has its own RCCL stream and the two directions of a 2-stage ring can
+  never serialise behind each other (no cross-edge deadlock).  In an 8x
+  MI355X node each edge is one direct xGMI link.  Sends/recvs are async:
+  `irecv` for the next microbatch is posted before the current one is
+  computed, and `Work.wait()` only makes the compute stream wait on the comm
+  stream (no host sync).
+* `GlooTransport` -- same protocol over gloo; device tensors are staged
+  through host memory.  Used for multi-process CPU tests and for rehearsing
+  the multi-rank engine on a single GPU.
+* `LocalTransport` -- in-process queues between stage threads (fake
+  transport for protocol tests), with optional fault injection.
+
+Ordering contract (what makes it deadlock-free): on every edge the sender
+posts sends in (step, microbatch) order and the receiver posts receives in
+the same order; no stage ever waits on an edge before posting the ops it
+owes on an earlier item.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import time
+from typing import Dict, List, Optional
+
+import torch
+
+
+class TransportError(RuntimeError):
+    pass
+
+
+class Handle:
+    """Result of an async receive: `.wait()` returns the tensor."""
+
+    def __init__(self, tensor: torch.Tensor, work=None, post=None):
+        self.tensor, self._work, self._post = tensor, work, post
+
+    def wait(self) -> torch.Tensor:
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        if self._post is not None:
+            self._post()
+            self._post = None
+        return self.tensor
+
+
+class SendHandle:
+    def __init__(self, work=None):
+        self._work = work
+
+    def wait(self) -> None:
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+
+
+class Transport:
+    rank: int = 0
+    world: int = 1
+
+    def send(self, t: torch.Tensor, dst: int, edge: str) -> SendHandle:
+        raise NotImplementedError
+
+    def irecv(self, out: torch.Tensor, src: int, edge: str) -> Handle:
+        raise NotImplementedError
+
+    def broadcast_object(self, obj, src: int = 0):
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        pass
+
+    def close(self) -> None:
+        pass
+
+
+# ---------------------------------------------------------------------------
+# torch.distributed transports
+# ---------------------------------------------------------------------------
+
+class _DistTransport(Transport):
+    def __init__(self, num_stages: int):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        if self.world != num_stages:
+            raise TransportError(f"world size {self.world} != num_stages {num_stages}")
+        # Groups must be created by every rank in the same order.
+        self.groups: Dict[str, object] = {}
+        P = num_stages
+        for i in range(P - 1):
+            self.groups[f"fwd{i}"] = dist.new_group([i, i + 1], backend=self._backend())
+        if P > 1:
+            self.groups["ret"] = dist.new_group([P - 1, 0], backend=self._backend())
+        self.ctrl = dist.new_group(list(range(P)), backend="gloo")
+
+    def _backend(self) -> str:
+        raise NotImplementedError
+
+    def _edge_group(self, edge: str, src: int, dst: int):
+        if edge == "fwd":
+            return self.groups[f"fwd{min(src, dst)}"]
+        return self.groups["ret"]
+
+    def broadcast_object(self, obj, src: int = 0):
+        lst = [obj]
+        self.dist.broadcast_object_list(lst, src=src, group=self.ctrl)
+        return lst[0]
+
+    def barrier(self) -> None:
+        self.dist.barrier(group=self.ctrl)
+
+
+class NcclTransport(_DistTransport):
+    """RCCL point-to-point over xGMI (backend 'nccl' IS RCCL on ROCm)."""
+
+    def _backend(self) -> str:
+        return "nccl"
+
+    def warmup(self, device) -> None:
+        """Eagerly create every edge communicator in a fixed global order so no
+        rank blocks in a lazy ncclCommInitRank while its peer waits elsewhere."""
+        dev = torch.device(device)
+        for name, g in self.groups.items():
+            members = self._members(name)
+            if self.rank in members:
+                t = torch.ones(1, device=dev)
+                self.dist.all_reduce(t, group=g)
+        torch.cuda.synchronize(dev)
+        self.barrier()
+
+    def _members(self, name: str) -> List[int]:
+        if name == "ret":
+            return [self.world - 1, 0]
+        i = int(name[3:])
+        return [i, i + 1]
+
+    def send(self, t, dst, edge):
+        g = self._edge_group(edge, self.rank, dst)
+        return SendHandle(self.dist.isend(t, dst, group=g))
+
+    def irecv(self, out, src, edge):
+        g = self._edge_group(edge, src, self.rank)
+        return Handle(out, self.dist.irecv(out, src, group=g))
+
+
+class GlooTransport(_DistTransport):
+    """Same protocol over gloo; device tensors are staged via host memory."""
+
+    def _backend(self) -> str:
+        return "gloo"
+
+    def send(self, t, dst, edge):
+        g = self._edge_group(edge, self.rank, dst)
+        host = t.detach().to("cpu", copy=True) if t.device.type != "cpu" else t.detach().clone()
+        return SendHandle(self.dist.isend(host, dst, group=g))
+
+    def irecv(self, out, src, edge):
+        g = self._edge_group(edge, src, self.rank)
+        if out.device.type == "cpu":
+            return Handle(out, self.dist.irecv(out, src, group=g))
+        host = torch.empty(out.shape, dtype=out.dtype)
+        work = self.dist.irecv(host, src, group=g)
+        return Handle(out, work, post=lambda: out.copy_(host))
+
+
+# ---------------------------------------------------------------------------
+# In-process fake transport (tests, single-process multi-stage)
+# ---------------------------------------------------------------------------
+
+class LocalFabric:
+    """Shared mailbox for P in-process stages.  fault: optional callable
+    (edge, src, dst, seq) -> None | "drop" | float(delay seconds) | Exception."""
+
+    def __init__(self, num_stages: int, timeout: float = 60.0, fault=None):
+        self.P = num_stages
+        self.timeout = timeout
+        self.fault = fault
+        self._q: Dict[tuple, queue.Queue] = {}
+        self._lock = threading.Lock()
+        self._bcast: Dict[int, queue.Queue] = {r: queue.Queue() for r in range(num_stages)}
+        self._seq: Dict[tuple, int] = {}
+        self._barrier = threading.Barrier(num_stages)
+
+    def q(self, key) -> queue.Queue:
+        with self._lock:
+            if key not in self._q:
+                self._q[key] = queue.Queue()
+            return self._q[key]
+
+    def next_seq(self, key) -> int:
+        with self._lock:
+            n = self._seq.get(key, 0)
+            self._seq[key] = n + 1
+            return n
+
+    def transport(self, rank: int) -> "LocalTransport":
+        return LocalTransport(self, rank)
+
+
+class LocalTransport(Transport):
+    def __init__(self, fabric: LocalFabric, rank: int):
+        self.fabric, self.rank, self.world = fabric, rank, fabric.P
+
+    def send(self, t, dst, edge):
+        key = (edge, self.rank, dst)
+        seq = self.fabric.next_seq(key)
+        payload = t.detach().clone()
+        if t.is_cuda:
+            torch.cuda.current_stream(t.device).synchronize()
+        f = self.fabric.fault(edge, self.rank, dst, seq) if self.fabric.fault else None
+        if isinstance(f, Exception):
+            raise f
+        if f == "drop":
+            return SendHandle()
+        if isinstance(f, (int, float)) and f > 0:
+            time.sleep(f)
+        self.fabric.q(key).put(payload)
+        return SendHandle()
+
+    def irecv(self, out, src, edge):
+        key = (edge, src, self.rank)
+        fabric = self.fabric
+
+        def post():
+            try:
+                t = fabric.q(key).get(timeout=fabric.timeout)
+            except queue.Empty:
+                raise TransportError(f"stage {self.rank}: timed out after {fabric.timeout}s "
+                                     f"waiting on {edge} from stage {src}") from None
+            out.copy_(t)
+
+        return Handle(out, None, post=post)
+
+    def broadcast_object(self, obj, src: int = 0):
+        if self.rank == src:
+            for r in range(self.world):
+                if r != src:
+                    self.fabric._bcast[r].put(obj)
+            return obj
+        return self.fabric._bcast[self.rank].get(timeout=self.fabric.timeout)
+
+    def barrier(self) -> None:
+        self.fabric._barrier.wait(timeout=self.fabric.timeout)
+
+
+def init_distributed(backend: str, device_type: str) -> None:
+    """Initialise torch.distributed from torchrun env vars (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR/PORT).  Binds the process to its GPU first."""
+    import os
+
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        return
+    kw = {}
+    if device_type == "cuda":
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        kw["device_id"] = torch.device("cuda", local)
+    dist.init_process_group(backend=backend, **kw)
+
+
+def make_dist_transport(num_stages: int, kind: str, device) -> Transport:
+    if kind == "nccl":
+        t = NcclTransport(num_stages)
+        t.warmup(device)
+        return t
+    if kind == "gloo":
+        t = GlooTransport(num_stages)
+        t.barrier()
+        return t
+    raise ValueError(f"unknown transport {kind!r}")
