@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Headline benchmark: output tokens/s + p50 per-token latency of the GPT-2
+pipeline at N stages = N MI355X (BASELINE.json "metric").
+
+One step = one complete generation round, end to end: prefill of every
+prompt, then `--gen` decode steps, for a global batch of N x --batch
+sequences split into microbatches that flow through the N-stage pipeline
+(one stage per GPU, RCCL p2p between stages).  Weak scaling: each GPU holds
+1/N of the layers and the global batch grows with N.  Nothing is skipped in
+the timed region: prefill, every layer, lm_head and the sampler (reference
+sampler: T=0.6, top-k=40; --greedy for argmax) run for every token.
+
+Data: synthetic random prompts, random-init weights of the named architecture
+(no network in this environment).
+
+Usage:  python bench.py [--gpus N --steps K --warmup W]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import statistics
+import sys
+import time
+
+# Reference measurements (reference server.py path on CPU): tok/s
+REFERENCE_TOK_S = {"gpt2": 0.69, "tiny-gpt2": 0.69, "gpt2-xl": 0.42}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--model", default="gpt2-xl")
+    p.add_argument("--batch", type=int, default=64, help="sequences per GPU (per microbatch)")
+    p.add_argument("--prompt", type=int, default=128)
+    p.add_argument("--gen", type=int, default=128)
+    p.add_argument("--microbatches", type=int, default=0, help="0 -> N (one per stage)")
+    p.add_argument("--greedy", action="store_true")
+    p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    import torch
+
+    from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
+    from llm_sharding_demo_amd.runtime.engine import Engine
+
+    N = args.gpus
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != N:
+        raise SystemExit(f"--gpus {N} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    M = args.microbatches or N
+    B = N * args.batch
+    cfg = EngineConfig(model_id=args.model, num_stages=N, max_batch=B,
+                       max_seq_len=args.prompt + args.gen, device="cuda",
+                       use_graphs=not args.no_graphs, num_microbatches=M, seed=args.seed,
+                       transport="nccl")
+    eng = Engine(cfg, mode="dist" if N > 1 else "local")
+    rank = eng.rank
+    worker = eng.workers[0]
+
+    rnd = random.Random(args.seed)
+    vocab = cfg.model.vocab_size
+    prompts = [[rnd.randrange(vocab) for _ in range(args.prompt)] for _ in range(B)]
+    sp = SamplingParams(greedy=args.greedy, temperature=0.6, top_k=40,
+                        max_new_tokens=args.gen, seed=1234)
+    slots = list(range(B))
+    # every rank builds the identical round spec (deterministic), no broadcast
+    eng._rng = random.Random(args.seed)
+    spec = eng.make_round(prompts, [sp] * B, slots, microbatches=M, record_timing=(rank == 0))
+
+    def barrier():
+        if N > 1:
+            eng.transport.barrier()
+
+    for _ in range(args.warmup):
+        worker.run_round(spec)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step_ms = []
+    for _ in range(args.steps):
+        res = worker.run_round(spec)
+        if rank == 0 and res is not None:
+            step_ms += res.step_times_ms
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if N > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=eng.transport.ctrl)
+        elapsed = float(t[0])
+    if rank == 0:
+        ms_per_step = elapsed * 1e3 / args.steps
+        tokens = B * args.gen * args.steps
+        value = tokens / elapsed
+        p50 = statistics.median(step_ms) if step_ms else None
+        base = REFERENCE_TOK_S.get(args.model)
+        out = {
+            "metric": "output tokens/sec + p50 per-token latency, GPT-2 pipeline at N MI355X",
+            "value": round(value, 2), "unit": "tokens/s", "n_gpus": N, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / base, 1) if base else None,
+            "dtype": "bf16", "data": "synthetic prompts, random-init weights",
+            "p50_token_latency_ms": round(p50, 4) if p50 is not None else None,
+            "config": {"model": args.model, "global_batch": B, "seq_len": args.prompt + args.gen,
+                       "prompt_len": args.prompt, "gen_tokens": args.gen, "microbatches": M,
+                       "parallelism": f"pp{N}", "sampler": "greedy" if args.greedy else "T0.6/top-k40",
+                       "hipgraphs": not args.no_graphs},
+        }
+        print(json.dumps(out), flush=True)
+    if N > 1:
+        eng.transport.barrier()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

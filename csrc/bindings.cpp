@@ -1,0 +1,352 @@
+// PyTorch bindings for the CDNA4 kernels (csrc/kernels/*.hip).
+//
+// Every entry point validates dtypes, shapes, strides and alignment on the
+// host before launching, so a bad call raises a Python exception instead of
+// faulting the GPU.  Launches go on the current HIP stream (graph-capturable:
+// no allocation-free syncs, no host<->device copies inside).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <hip/hip_runtime.h>
+#include <cmath>
+
+#include "kernels/gemm_params.h"
+
+typedef lsd_bf16_t bf16;
+using lsd::GemmParams;
+
+extern "C" {
+hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, hipStream_t st);
+hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte, const bf16* wpe, float* out,
+                     int T, int H, int vocab, hipStream_t st);
+hipError_t lsd_norm(float* x, const float* slab, int splits, const bf16* pbias, const bf16* w,
+                    const bf16* b, bf16* out, int T, int H, float eps, int rms, const int* rows,
+                    int nrows, hipStream_t st);
+hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
+                           const int* seq_slots, const int* qpos, bf16* out, long ldo,
+                           float* part_o, float* part_ml, int B, int nh, int n_kv, int hd,
+                           int max_seq, int splits, float scale_log2, hipStream_t st);
+hipError_t lsd_attn_prefill(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
+                            const int* tiles, int n_tiles, const int* seq_slots,
+                            const int* q_start, const int* cu_q, bf16* out, long ldo, int nh,
+                            int n_kv, int hd, int max_seq, float scale_log2, hipStream_t st);
+hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
+                      const int* topk, const int* greedy, const long long* seeds,
+                      const long long* step, int* out, hipStream_t st);
+}
+
+namespace {
+
+enum Epi : int { EPI_BF16 = 0, EPI_GELU = 1, EPI_SILU_MUL = 2, EPI_F32 = 3, EPI_RESID = 4,
+                 EPI_SLAB = 5, EPI_QKV = 6 };
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
+}
+
+void need(const torch::Tensor& t, c10::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+
+void need_rows(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with unit last stride");
+  TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8 elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+const bf16* bptr(const torch::Tensor& t) { return reinterpret_cast<const bf16*>(t.data_ptr()); }
+bf16* bptr_mut(const torch::Tensor& t) { return reinterpret_cast<bf16*>(t.data_ptr()); }
+
+const bf16* opt_bias(const c10::optional<torch::Tensor>& b, int N) {
+  if (!b.has_value()) return nullptr;
+  need(*b, torch::kBFloat16, "bias");
+  TORCH_CHECK(b->is_contiguous() && b->numel() == N, "bias must be contiguous [N]");
+  return bptr(*b);
+}
+
+GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, bool tiled) {
+  need(a, torch::kBFloat16, "a");
+  need(w, torch::kBFloat16, "w");
+  need_rows(a, "a");
+  need_rows(w, "w");
+  TORCH_CHECK(a.size(1) == w.size(1), "K mismatch: a ", a.sizes(), " w ", w.sizes());
+  GemmParams p{};
+  p.A = bptr(a); p.lda = a.stride(0);
+  p.W = bptr(w); p.ldw = w.stride(0);
+  p.M = a.size(0); p.N = w.size(0); p.K = a.size(1);
+  p.splits = 1;
+  TORCH_CHECK(p.N % 16 == 0, "N must be a multiple of 16 (pad the weight), got ", p.N);
+  if (tiled) {
+    TORCH_CHECK(p.K % 64 == 0, "tiled GEMM needs K % 64 == 0, got ", p.K);
+  } else {
+    TORCH_CHECK(p.M >= 1 && p.M <= 64, "skinny GEMM needs 1 <= M <= 64, got ", p.M);
+    TORCH_CHECK(p.K % 32 == 0, "skinny GEMM needs K % 32 == 0, got ", p.K);
+  }
+  return p;
+}
+
+int check_splits(int splits, const GemmParams& p, bool tiled) {
+  const int kt = tiled ? p.K / 64 : p.K / 32;
+  TORCH_CHECK(splits >= 1 && splits <= kt, "splits must be in [1, ", kt, "], got ", splits);
+  return splits;
+}
+
+// out = act(a @ w^T + bias), bf16
+torch::Tensor linear(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,
+                     int64_t act, bool tiled) {
+  GemmParams p = base_params(a, w, tiled);
+  p.bias = opt_bias(bias, p.N);
+  int epi = act == 1 ? EPI_GELU : (act == 2 ? EPI_SILU_MUL : EPI_BF16);
+  if (epi == EPI_SILU_MUL) TORCH_CHECK(p.N % 32 == 0, "silu_mul needs N % 32 == 0");
+  const int n_out = epi == EPI_SILU_MUL ? p.N / 2 : p.N;
+  auto out = torch::empty({p.M, n_out}, a.options());
+  if (p.M == 0) return out;
+  p.out = out.data_ptr(); p.ldo = n_out;
+  check_hip(lsd_gemm(&p, epi, tiled, cur_stream()), "linear");
+  return out;
+}
+
+// fp32 logits = a @ w^T
+torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, bool tiled) {
+  GemmParams p = base_params(a, w, tiled);
+  auto out = torch::empty({p.M, p.N}, a.options().dtype(torch::kFloat32));
+  if (p.M == 0) return out;
+  p.out = out.data_ptr(); p.ldo = p.N;
+  check_hip(lsd_gemm(&p, EPI_F32, tiled, cur_stream()), "linear_f32");
+  return out;
+}
+
+// x += a @ w^T + bias (splits == 1) or return fp32 slabs [splits, M, N] to be
+// folded in by the next norm (splits > 1).
+c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
+                                              c10::optional<torch::Tensor> bias, torch::Tensor x,
+                                              int64_t splits, bool tiled) {
+  GemmParams p = base_params(a, w, tiled);
+  need(x, torch::kFloat32, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(0) == p.M && x.size(1) == p.N,
+              "residual x must be contiguous [M, N]");
+  p.splits = check_splits(splits, p, tiled);
+  if (p.M == 0) return c10::nullopt;
+  if (p.splits == 1) {
+    p.bias = opt_bias(bias, p.N);
+    p.out = x.data_ptr(); p.ldo = p.N;
+    check_hip(lsd_gemm(&p, EPI_RESID, tiled, cur_stream()), "linear_residual");
+    return c10::nullopt;
+  }
+  auto slab = torch::empty({p.splits, p.M, p.N}, x.options());
+  p.slab = slab.data_ptr<float>();
+  check_hip(lsd_gemm(&p, EPI_SLAB, tiled, cur_stream()), "linear_residual(split)");
+  return slab;
+}
+
+// QKV projection: returns q bf16 [M, q_size]; k, v written into the caches.
+torch::Tensor linear_qkv(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,
+                         torch::Tensor kc, torch::Tensor vc, torch::Tensor tslot,
+                         torch::Tensor tpos, int64_t q_size, int64_t kv_size, int64_t hd,
+                         c10::optional<torch::Tensor> rope, bool tiled) {
+  GemmParams p = base_params(a, w, tiled);
+  p.bias = opt_bias(bias, p.N);
+  need(kc, torch::kBFloat16, "k_cache");
+  need(vc, torch::kBFloat16, "v_cache");
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.sizes() == kc.sizes() && vc.is_contiguous(),
+              "caches must be contiguous [slots, n_kv, max_seq, hd]");
+  TORCH_CHECK(kc.size(3) == hd && kc.size(1) * hd == kv_size, "cache shape mismatch");
+  TORCH_CHECK(p.N == q_size + 2 * kv_size, "w rows must be q_size + 2*kv_size");
+  TORCH_CHECK(q_size % hd == 0 && hd % 16 == 0, "bad head dims");
+  need(tslot, torch::kInt32, "token_slots");
+  need(tpos, torch::kInt32, "token_pos");
+  TORCH_CHECK(tslot.numel() == p.M && tpos.numel() == p.M && tslot.is_contiguous() &&
+              tpos.is_contiguous(), "token_slots/token_pos must be contiguous [M]");
+  p.kc = bptr_mut(kc); p.vc = bptr_mut(vc);
+  p.tslot = tslot.data_ptr<int>(); p.tpos = tpos.data_ptr<int>();
+  p.q_size = q_size; p.kv_size = kv_size; p.hd = hd;
+  p.max_seq = kc.size(2); p.n_kv = kc.size(1);
+  if (rope.has_value()) {
+    need(*rope, torch::kFloat32, "rope");
+    TORCH_CHECK(rope->is_contiguous() && rope->dim() == 3 && rope->size(1) == hd / 2 &&
+                rope->size(2) == 2 && rope->size(0) >= p.max_seq, "rope table must be [>=max_seq, hd/2, 2]");
+    p.rope = rope->data_ptr<float>();
+  }
+  auto q = torch::empty({p.M, q_size}, a.options());
+  if (p.M == 0) return q;
+  p.out = q.data_ptr(); p.ldo = q_size;
+  check_hip(lsd_gemm(&p, EPI_QKV, tiled, cur_stream()), "linear_qkv");
+  return q;
+}
+
+torch::Tensor embed(torch::Tensor ids, torch::Tensor pos, torch::Tensor wte,
+                    c10::optional<torch::Tensor> wpe) {
+  need(ids, torch::kInt32, "ids");
+  need(pos, torch::kInt32, "pos");
+  need(wte, torch::kBFloat16, "wte");
+  TORCH_CHECK(ids.is_contiguous() && pos.is_contiguous() && ids.numel() == pos.numel(), "ids/pos");
+  TORCH_CHECK(wte.dim() == 2 && wte.is_contiguous() && wte.size(1) % 8 == 0, "wte [V, H], H % 8 == 0");
+  const int T = ids.numel(), H = wte.size(1);
+  const bf16* pe = nullptr;
+  if (wpe.has_value()) {
+    need(*wpe, torch::kBFloat16, "wpe");
+    TORCH_CHECK(wpe->is_contiguous() && wpe->size(1) == H, "wpe [P, H]");
+    pe = bptr(*wpe);
+  }
+  auto out = torch::empty({T, H}, wte.options().dtype(torch::kFloat32));
+  check_hip(lsd_embed(ids.data_ptr<int>(), pos.data_ptr<int>(), bptr(wte), pe,
+                      out.data_ptr<float>(), T, H, wte.size(0), cur_stream()), "embed");
+  return out;
+}
+
+c10::optional<torch::Tensor> norm(torch::Tensor x, c10::optional<torch::Tensor> slab,
+                                  c10::optional<torch::Tensor> pbias, c10::optional<torch::Tensor> w,
+                                  c10::optional<torch::Tensor> b, double eps, bool rms,
+                                  c10::optional<torch::Tensor> rows, bool want_out) {
+  need(x, torch::kFloat32, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be contiguous [T, H]");
+  const int T = x.size(0), H = x.size(1);
+  TORCH_CHECK(H % 4 == 0 && H <= 8192, "norm needs H % 4 == 0 and H <= 8192");
+  const bf16* wp = nullptr;
+  if (want_out) {
+    TORCH_CHECK(w.has_value(), "norm output needs a weight");
+    need(*w, torch::kBFloat16, "w");
+    TORCH_CHECK(w->numel() == H, "w [H]");
+    wp = bptr(*w);
+    if (!rms) {
+      TORCH_CHECK(b.has_value(), "layernorm needs a bias");
+      need(*b, torch::kBFloat16, "b");
+      TORCH_CHECK(b->numel() == H, "b [H]");
+    }
+  }
+  const float* sp = nullptr;
+  int splits = 0;
+  if (slab.has_value()) {
+    need(*slab, torch::kFloat32, "slab");
+    TORCH_CHECK(slab->is_contiguous() && slab->dim() == 3 && slab->size(1) == T && slab->size(2) == H,
+                "slab must be [S, T, H]");
+    sp = slab->data_ptr<float>();
+    splits = slab->size(0);
+  }
+  const bf16* pb = nullptr;
+  if (pbias.has_value()) {
+    TORCH_CHECK(sp != nullptr, "pending bias without slab");
+    need(*pbias, torch::kBFloat16, "pending_bias");
+    TORCH_CHECK(pbias->numel() == H, "pending bias [H]");
+    pb = bptr(*pbias);
+  }
+  const int* rp = nullptr;
+  int n = T;
+  if (rows.has_value()) {
+    need(*rows, torch::kInt32, "rows");
+    TORCH_CHECK(sp == nullptr, "row gather cannot combine slabs");
+    TORCH_CHECK(rows->is_contiguous(), "rows must be contiguous");
+    rp = rows->data_ptr<int>();
+    n = rows->numel();
+  }
+  c10::optional<torch::Tensor> out;
+  bf16* op = nullptr;
+  if (want_out) {
+    out = torch::empty({n, H}, x.options().dtype(torch::kBFloat16));
+    op = bptr_mut(*out);
+  }
+  check_hip(lsd_norm(x.data_ptr<float>(), sp, splits, pb, wp, (want_out && b.has_value()) ? bptr(*b) : nullptr,
+                     op, T, H, (float)eps, rms ? 1 : 0, rp, n, cur_stream()), "norm");
+  return out;
+}
+
+void check_cache(const torch::Tensor& kc, const torch::Tensor& vc) {
+  need(kc, torch::kBFloat16, "k_cache");
+  need(vc, torch::kBFloat16, "v_cache");
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && kc.sizes() == vc.sizes(),
+              "caches must be contiguous [slots, n_kv, max_seq, hd]");
+}
+
+torch::Tensor attn_decode(torch::Tensor q, torch::Tensor kc, torch::Tensor vc,
+                          torch::Tensor seq_slots, torch::Tensor qpos, int64_t nh,
+                          int64_t splits) {
+  need(q, torch::kBFloat16, "q");
+  need_rows(q, "q");
+  check_cache(kc, vc);
+  const int B = q.size(0), n_kv = kc.size(1), hd = kc.size(3);
+  TORCH_CHECK(q.size(1) == nh * hd && nh % n_kv == 0, "q must be [B, nh*hd]");
+  TORCH_CHECK(hd == 64 || hd == 128, "head_dim must be 64 or 128");
+  need(seq_slots, torch::kInt32, "seq_slots");
+  need(qpos, torch::kInt32, "qpos");
+  TORCH_CHECK(seq_slots.numel() == B && qpos.numel() == B, "seq_slots/qpos [B]");
+  TORCH_CHECK(splits >= 1 && splits <= 256, "splits in [1, 256]");
+  auto out = torch::empty({B, nh * hd}, q.options());
+  torch::Tensor po, pml;
+  float* pop = nullptr;
+  float* pmlp = nullptr;
+  if (splits > 1) {
+    po = torch::empty({B, nh, splits, hd}, q.options().dtype(torch::kFloat32));
+    pml = torch::empty({B, nh, splits, 2}, q.options().dtype(torch::kFloat32));
+    pop = po.data_ptr<float>();
+    pmlp = pml.data_ptr<float>();
+  }
+  const float sl2 = 1.4426950408889634f / std::sqrt((float)hd);
+  check_hip(lsd_attn_decode(bptr(q), q.stride(0), bptr(kc), bptr(vc), seq_slots.data_ptr<int>(),
+                            qpos.data_ptr<int>(), bptr_mut(out), out.stride(0), pop, pmlp, B, nh,
+                            n_kv, hd, kc.size(2), splits, sl2, cur_stream()), "attn_decode");
+  return out;
+}
+
+torch::Tensor attn_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc,
+                           torch::Tensor tiles, torch::Tensor seq_slots, torch::Tensor q_start,
+                           torch::Tensor cu_q, int64_t nh) {
+  need(q, torch::kBFloat16, "q");
+  need_rows(q, "q");
+  check_cache(kc, vc);
+  const int n_kv = kc.size(1), hd = kc.size(3);
+  TORCH_CHECK(q.size(1) == nh * hd && nh % n_kv == 0, "q must be [T, nh*hd]");
+  TORCH_CHECK(hd == 64 || hd == 128, "head_dim must be 64 or 128");
+  need(tiles, torch::kInt32, "tiles");
+  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 2 && tiles.is_contiguous(), "tiles [n, 2]");
+  need(seq_slots, torch::kInt32, "seq_slots");
+  need(q_start, torch::kInt32, "q_start");
+  need(cu_q, torch::kInt32, "cu_q");
+  TORCH_CHECK(cu_q.numel() == seq_slots.numel() + 1, "cu_q [B+1]");
+  auto out = torch::empty_like(q);
+  const float sl2 = 1.4426950408889634f / std::sqrt((float)hd);
+  check_hip(lsd_attn_prefill(bptr(q), q.stride(0), bptr(kc), bptr(vc), tiles.data_ptr<int>(),
+                             tiles.size(0), seq_slots.data_ptr<int>(), q_start.data_ptr<int>(),
+                             cu_q.data_ptr<int>(), bptr_mut(out), out.stride(0), nh, n_kv, hd,
+                             kc.size(2), sl2, cur_stream()), "attn_prefill");
+  return out;
+}
+
+torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
+                     torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step) {
+  need(logits, torch::kFloat32, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && V <= logits.size(1) && V >= 1, "logits [B, >=V]");
+  const int B = logits.size(0);
+  need(temp, torch::kFloat32, "temperature");
+  need(topk, torch::kInt32, "top_k");
+  need(greedy, torch::kInt32, "greedy");
+  need(seeds, torch::kInt64, "seeds");
+  need(step, torch::kInt64, "step");
+  TORCH_CHECK(temp.numel() == B && topk.numel() == B && greedy.numel() == B && seeds.numel() == B &&
+              step.numel() == B, "sampling params must be [B]");
+  auto out = torch::empty({B}, logits.options().dtype(torch::kInt32));
+  check_hip(lsd_sample(logits.data_ptr<float>(), logits.stride(0), B, V, temp.data_ptr<float>(),
+                       topk.data_ptr<int>(), greedy.data_ptr<int>(),
+                       reinterpret_cast<const long long*>(seeds.data_ptr<int64_t>()),
+                       reinterpret_cast<const long long*>(step.data_ptr<int64_t>()),
+                       out.data_ptr<int>(), cur_stream()), "sample");
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "CDNA4 (gfx950) kernels for llm_sharding_demo_amd";
+  m.def("linear", &linear);
+  m.def("linear_f32", &linear_f32);
+  m.def("linear_residual", &linear_residual);
+  m.def("linear_qkv", &linear_qkv);
+  m.def("embed", &embed);
+  m.def("norm", &norm);
+  m.def("attn_decode", &attn_decode);
+  m.def("attn_prefill", &attn_prefill);
+  m.def("sample", &sample);
+  m.attr("arch") = "gfx950";
+}

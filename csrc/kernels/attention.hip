@@ -1,0 +1,394 @@
+// Causal attention over the shard-local KV cache.
+//
+// K7 of SURVEY.md §2.5 (`[tf5.15] modeling_gpt2.py:201-220`, SDPA causal):
+//   softmax(Q K^T / sqrt(hd) + causal) V.  The reference recomputes attention
+// over the whole sequence every step and gets causality only implicitly
+// (quirk Q3); here the mask is explicit and K/V come from the cache.
+//
+// Cache layout [slot][kv_head][position][hd] (bf16): one (slot, head) is a
+// contiguous run of positions, so every key/value row read is part of one
+// linear stream.
+//
+// attn_decode : one query per sequence (decode).  Memory-bound flash-decoding:
+//   block = (sequence, kv head[, key split]); 4 waves stride over the keys; a
+//   key row (hd*2 bytes) is read by hd/8 lanes with 16-byte loads, so each
+//   wave-instruction streams 1 KiB of contiguous K (then V).  GQA: the G query
+//   heads sharing a kv head are served from the same K/V loads.  Online
+//   softmax in exp2 domain; waves/splits merged with (m, l) rescaling.
+// attn_prefill: packed ragged queries (prefill / chunked prefill).  MFMA
+//   16x16x32 bf16 with SWAPPED operands: S^T = K . Q^T puts one query per lane
+//   (column) so the row max/sum are lane-local plus a 2-step exchange, and the
+//   S^T accumulator registers ARE the P^T B-operand of the PV MFMA (no LDS
+//   round trip for P).  V^T fragments come from the row-major V tile via the
+//   gfx950 hardware transpose read ds_read_b64_tr_b16.
+#include "common.h"
+
+namespace lsd {
+
+constexpr float NEG = -1e30f;
+
+template <int HD, int G, int U>
+__global__ __launch_bounds__(256) void attn_decode_kernel(
+    const bf16* __restrict__ q, long ldq, const bf16* __restrict__ kc,
+    const bf16* __restrict__ vc, const int* __restrict__ seq_slots,
+    const int* __restrict__ qpos, bf16* out, long ldo, float* part_o, float* part_ml, int n_kv,
+    int max_seq, int splits, float scale_log2) {
+  constexpr int LPK = HD / 8;    // lanes per key row
+  constexpr int KPI = 64 / LPK;  // keys per wave-instruction
+  const int b = blockIdx.x / n_kv, kvh = blockIdx.x % n_kv, split = blockIdx.y;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int ds = lane % LPK, kg = lane / LPK;
+  const int ctx = qpos[b] + 1;
+  const int per = (ctx + splits - 1) / splits;
+  const int k_lo = split * per, k_hi = min(ctx, k_lo + per);
+  const long base = ((long)seq_slots[b] * n_kv + kvh) * (long)max_seq * HD + ds * 8;
+
+  float qf[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    bf16x8 qq = ld8(q + (long)b * ldq + (long)(kvh * G + g) * HD + ds * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[g][j] = bf2f(qq[j]) * scale_log2;
+  }
+  float m[G], l[G], o[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m[g] = NEG;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
+  }
+
+  for (int c0 = k_lo + w * KPI; c0 < k_hi; c0 += 4 * KPI * U) {
+    bf16x8 kv[U];
+    int key[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      key[u] = c0 + u * 4 * KPI + kg;
+      const int kk = min(key[u], k_hi - 1);
+      kv[u] = ld8(kc + base + (long)kk * HD);
+    }
+    float s[G][U];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += qf[g][j] * bf2f(kv[u][j]);
+#pragma unroll
+        for (int msk = 1; msk < LPK; msk <<= 1) acc += shfl_xor(acc, msk);
+        s[g][u] = key[u] < k_hi ? acc : NEG;
+      }
+    bf16x8 vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) vv[u] = ld8(vc + base + (long)min(key[u], k_hi - 1) * HD);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float mx = s[g][0];
+#pragma unroll
+      for (int u = 1; u < U; ++u) mx = fmaxf(mx, s[g][u]);
+      const float mn = fmaxf(m[g], mx);
+      const float alpha = exp2f(m[g] - mn);
+      float p[U], ps = 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        p[u] = exp2f(s[g][u] - mn);
+        ps += p[u];
+      }
+      l[g] = l[g] * alpha + ps;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = o[g][j] * alpha;
+#pragma unroll
+        for (int u = 0; u < U; ++u) a += p[u] * bf2f(vv[u][j]);
+        o[g][j] = a;
+      }
+      m[g] = mn;
+    }
+  }
+
+  // merge the key groups of this wave (lanes with equal ds)
+#pragma unroll
+  for (int msk = LPK; msk < 64; msk <<= 1) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float mo = shfl_xor(m[g], msk), lo = shfl_xor(l[g], msk);
+      const float mn = fmaxf(m[g], mo);
+      const float a = exp2f(m[g] - mn), bb = exp2f(mo - mn);
+      l[g] = l[g] * a + lo * bb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + shfl_xor(o[g][j], msk) * bb;
+      m[g] = mn;
+    }
+  }
+  // merge the 4 waves through LDS
+  __shared__ float sm[4][G][LPK][10];
+  if (kg == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      sm[w][g][ds][0] = m[g];
+      sm[w][g][ds][1] = l[g];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sm[w][g][ds][2 + j] = o[g][j];
+    }
+  }
+  __syncthreads();
+  if (w != 0 || kg != 0) return;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float mm = NEG;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) mm = fmaxf(mm, sm[ww][g][ds][0]);
+    float ll = 0.f, oo[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = exp2f(sm[ww][g][ds][0] - mm);
+      ll += sm[ww][g][ds][1] * f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) oo[j] += sm[ww][g][ds][2 + j] * f;
+    }
+    const int h = kvh * G + g;
+    if (splits == 1) {
+      const float inv = ll > 0.f ? 1.f / ll : 0.f;
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = f2bf(oo[j] * inv);
+      st8(out + (long)b * ldo + (long)h * HD + ds * 8, r);
+    } else {
+      const int nh = n_kv * G;
+      const long pi = ((long)b * nh + h) * splits + split;
+      float* po = part_o + pi * HD + ds * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) po[j] = oo[j];
+      if (ds == 0) {
+        part_ml[pi * 2] = mm;
+        part_ml[pi * 2 + 1] = ll;
+      }
+    }
+  }
+}
+
+// Merge split-K decode partials: one block per (sequence, head).
+template <int HD>
+__global__ __launch_bounds__(64) void attn_decode_combine_kernel(const float* part_o,
+                                                                 const float* part_ml, bf16* out,
+                                                                 long ldo, int nh, int splits) {
+  const int b = blockIdx.x / nh, h = blockIdx.x % nh;
+  const long p0 = ((long)b * nh + h) * splits;
+  float mm = NEG;
+  for (int s = 0; s < splits; ++s) mm = fmaxf(mm, part_ml[(p0 + s) * 2]);
+  for (int d = threadIdx.x; d < HD; d += 64) {
+    float ll = 0.f, oo = 0.f;
+    for (int s = 0; s < splits; ++s) {
+      const float f = exp2f(part_ml[(p0 + s) * 2] - mm);
+      ll += part_ml[(p0 + s) * 2 + 1] * f;
+      oo += part_o[(p0 + s) * HD + d] * f;
+    }
+    out[(long)b * ldo + (long)h * HD + d] = f2bf(ll > 0.f ? oo / ll : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Prefill: 64-query tile per block (4 waves x 16 queries), 64-key tiles in LDS
+// ---------------------------------------------------------------------------
+typedef short short4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x4 ds_read_tr(const bf16* lds_ptr) {
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds_ptr));
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_prefill_kernel(
+    const bf16* __restrict__ q, long ldq, const bf16* __restrict__ kc,
+    const bf16* __restrict__ vc, const int* __restrict__ tiles,
+    const int* __restrict__ seq_slots, const int* __restrict__ q_start,
+    const int* __restrict__ cu_q, bf16* out, long ldo, int nh, int n_kv, int max_seq,
+    float scale_log2) {
+  constexpr int KT = 64;              // keys per tile
+  constexpr int LDR = HD + 8;         // padded LDS row (elements): +16 B
+  constexpr int CPR = HD / 8;         // 16-B chunks per row
+  constexpr int CH = KT * CPR / 256;  // chunks per thread per tile
+  __shared__ __attribute__((aligned(16))) bf16 ks[KT * LDR];
+  __shared__ __attribute__((aligned(16))) bf16 vs[KT * LDR];
+
+  const int bseq = tiles[blockIdx.x * 2], qoff = tiles[blockIdx.x * 2 + 1];
+  const int h = blockIdx.y;
+  const int kvh = h / (nh / n_kv);
+  const int qlen = cu_q[bseq + 1] - cu_q[bseq];
+  const int st = q_start[bseq];
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int qi = qoff + w * 16 + r;  // this lane's query (row within the sequence)
+  const int qrow = cu_q[bseq] + min(qi, qlen - 1);
+  const int my_pos = st + qi;
+  const int kmax = st + min(qoff + 64, qlen);  // keys [0, kmax) are needed by the tile
+  const int ntile = (kmax + KT - 1) / KT;
+  const long base = ((long)seq_slots[bseq] * n_kv + kvh) * (long)max_seq * HD;
+
+  bf16x8 qf[HD / 32];
+#pragma unroll
+  for (int kk = 0; kk < HD / 32; ++kk) qf[kk] = ld8(q + (long)qrow * ldq + (long)h * HD + kk * 32 + g * 8);
+
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int di = 0; di < HD / 16; ++di) o[di] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = NEG, lsum = 0.f;
+
+  bf16x8 kreg[CH], vreg[CH];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = threadIdx.x + c * 256;
+      const int key = min(kt * KT + idx / CPR, kmax - 1);
+      const long off = base + (long)key * HD + (idx % CPR) * 8;
+      kreg[c] = ld8(kc + off);
+      vreg[c] = ld8(vc + off);
+    }
+  };
+  load_tile(0);
+  for (int kt = 0; kt < ntile; ++kt) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = threadIdx.x + c * 256;
+      st8(ks + (idx / CPR) * LDR + (idx % CPR) * 8, kreg[c]);
+      st8(vs + (idx / CPR) * LDR + (idx % CPR) * 8, vreg[c]);
+    }
+    __syncthreads();
+    if (kt + 1 < ntile) load_tile(kt + 1);  // in flight under this tile's math
+
+    // S^T[key][q] for 4 subtiles of 16 keys
+    f32x4 sacc[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      sacc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (ni * 16 + r) * LDR + kk * 32 + g * 8);
+        sacc[ni] = mfma16(kf, qf[kk], sacc[ni]);
+      }
+    }
+    // scale, causal mask, tile max (lane-local over 16 keys, then across g)
+    float tmax = NEG;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kt * KT + ni * 16 + 4 * g + i;
+        float sv = sacc[ni][i] * scale_log2;
+        sv = key <= my_pos ? sv : NEG;
+        sacc[ni][i] = sv;
+        tmax = fmaxf(tmax, sv);
+      }
+    tmax = fmaxf(tmax, shfl_xor(tmax, 16));
+    tmax = fmaxf(tmax, shfl_xor(tmax, 32));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = exp2f(sacc[ni][i] - mn);
+        sacc[ni][i] = p;
+        ps += p;
+      }
+    lsum = lsum * alpha + ps;
+#pragma unroll
+    for (int di = 0; di < HD / 16; ++di) o[di] *= alpha;
+    // O^T[d][q] += V^T[d][key] . P^T[key][q]; k-slot j of group g <-> key
+    // 32kk + 4g + j (j < 4), 32kk + 16 + 4g + (j - 4) (j >= 4)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = f2bf(sacc[2 * kk][j]);
+        pf[4 + j] = f2bf(sacc[2 * kk + 1][j]);
+      }
+      const int r0 = kk * 32 + 4 * g + (r >> 2);
+#pragma unroll
+      for (int di = 0; di < HD / 16; ++di) {
+        const int col = di * 16 + 4 * (r & 3);
+        bf16x4 lo = ds_read_tr(vs + r0 * LDR + col);
+        bf16x4 hi = ds_read_tr(vs + (r0 + 16) * LDR + col);
+        bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[di] = mfma16(vf, pf, o[di]);
+      }
+    }
+    __syncthreads();
+  }
+  lsum += shfl_xor(lsum, 16);
+  lsum += shfl_xor(lsum, 32);
+  if (qi < qlen) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* op = out + (long)qrow * ldo + (long)h * HD;
+#pragma unroll
+    for (int di = 0; di < HD / 16; ++di) {
+      bf16x4 rr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rr[i] = f2bf(o[di][i] * inv);
+      st4(op + di * 16 + 4 * g, rr);
+    }
+  }
+}
+
+}  // namespace lsd
+
+using namespace lsd;
+
+extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
+                                      const int* seq_slots, const int* qpos, bf16* out, long ldo,
+                                      float* part_o, float* part_ml, int B, int nh, int n_kv,
+                                      int hd, int max_seq, int splits, float scale_log2,
+                                      hipStream_t st) {
+  if (B == 0) return hipSuccess;
+  const int G = nh / n_kv;
+  dim3 grid(B * n_kv, splits), block(256);
+#define LSD_DEC(HDV, GV)                                                                      \
+  if (hd == HDV && G == GV) {                                                                 \
+    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 4>), grid, block, 0, st, q, ldq, kc, vc,  \
+                       seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq, splits,     \
+                       scale_log2);                                                           \
+    goto combine;                                                                             \
+  }
+  LSD_DEC(64, 1)
+  LSD_DEC(64, 2)
+  LSD_DEC(64, 4)
+  LSD_DEC(128, 1)
+  LSD_DEC(128, 2)
+  LSD_DEC(128, 4)
+  LSD_DEC(128, 8)
+#undef LSD_DEC
+  return hipErrorInvalidValue;
+combine:
+  if (splits > 1) {
+    if (hd == 64)
+      hipLaunchKernelGGL((attn_decode_combine_kernel<64>), dim3(B * nh), dim3(64), 0, st, part_o,
+                         part_ml, out, ldo, nh, splits);
+    else
+      hipLaunchKernelGGL((attn_decode_combine_kernel<128>), dim3(B * nh), dim3(64), 0, st, part_o,
+                         part_ml, out, ldo, nh, splits);
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t lsd_attn_prefill(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
+                                       const int* tiles, int n_tiles, const int* seq_slots,
+                                       const int* q_start, const int* cu_q, bf16* out, long ldo,
+                                       int nh, int n_kv, int hd, int max_seq, float scale_log2,
+                                       hipStream_t st) {
+  if (n_tiles == 0) return hipSuccess;
+  dim3 grid(n_tiles, nh), block(256);
+  if (hd == 64)
+    hipLaunchKernelGGL((attn_prefill_kernel<64>), grid, block, 0, st, q, ldq, kc, vc, tiles,
+                       seq_slots, q_start, cu_q, out, ldo, nh, n_kv, max_seq, scale_log2);
+  else if (hd == 128)
+    hipLaunchKernelGGL((attn_prefill_kernel<128>), grid, block, 0, st, q, ldq, kc, vc, tiles,
+                       seq_slots, q_start, cu_q, out, ldo, nh, n_kv, max_seq, scale_log2);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}

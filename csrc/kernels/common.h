@@ -1,0 +1,94 @@
+// Common CDNA4 (gfx950 / MI355X) helpers for the engine kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * wave64: lane = threadIdx.x & 63, all cross-lane reductions span 64 lanes
+//   * bf16 storage, fp32 math; 16-byte vector loads for every streamed tensor
+//   * MFMA: v_mfma_f32_16x16x32_bf16.  Operand maps (lane l, r = l & 15, g = l >> 4):
+//       A[row r][k = 8g + j]   B[k = 8g + j][col r]   (j = 0..7, one 16-byte fragment)
+//       C/D: col = r, row = 4g + i (i = 0..3)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lsd {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }  // v_cvt_pk_bf16_f32, RNE, NaN-safe
+
+// 16-byte loads/stores through an integer vector type (hipcc does not
+// auto-vectorise bf16 scalar loads: guide Guideline 13).
+__device__ __forceinline__ bf16x8 ld8(const bf16* p) {
+  u32x4 v = *reinterpret_cast<const u32x4*>(p);
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ void st8(bf16* p, bf16x8 v) {
+  *reinterpret_cast<u32x4*>(p) = __builtin_bit_cast(u32x4, v);
+}
+__device__ __forceinline__ bf16x4 ld4(const bf16* p) {
+  u32x2 v = *reinterpret_cast<const u32x2*>(p);
+  return __builtin_bit_cast(bf16x4, v);
+}
+__device__ __forceinline__ void st4(bf16* p, bf16x4 v) {
+  *reinterpret_cast<u32x2*>(p) = __builtin_bit_cast(u32x2, v);
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ T shfl_xor(T v, int m) { return __shfl_xor(v, m, 64); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, shfl_xor(v, m));
+  return v;
+}
+
+// Block-wide sum for blockDim.x = nwaves*64 (<= 1024); `red` holds >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane_id() == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// gelu_new (tanh approximation) -- [tf5.15] activations.py:59-66
+__device__ __forceinline__ float gelu_new(float x) {
+  const float c = 0.7978845608028654f;  // sqrt(2/pi)
+  float u = c * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+// Bijective XCD-aware remap of a 1-D workgroup id (guide §5.5 T1, "XCD
+// swizzle must be bijective"): consecutive logical tiles land on one XCD so
+// tiles sharing an operand panel share that XCD's L2.  Speed only.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  if (nwg < nx) return bid;
+  const int q = nwg / nx, r = nwg % nx, x = bid % nx;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / nx;
+}
+
+}  // namespace lsd

@@ -1,0 +1,27 @@
+// GEMM launch parameters shared by csrc/kernels/gemm.hip and csrc/bindings.cpp.
+#pragma once
+
+#if defined(__clang__)
+typedef __bf16 lsd_bf16_t;
+#else
+typedef unsigned short lsd_bf16_t;  // host-only: storage-compatible, pointers only
+#endif
+
+namespace lsd {
+
+struct GemmParams {
+  const lsd_bf16_t* A; long lda;
+  const lsd_bf16_t* W; long ldw;
+  int M, N, K;
+  const lsd_bf16_t* bias;
+  void* out; long ldo;
+  float* slab;
+  int splits;
+  // QKV epilogue
+  lsd_bf16_t* kc; lsd_bf16_t* vc;  // [slots][n_kv][max_seq][hd]
+  const int* tslot; const int* tpos;
+  int q_size, kv_size, hd, max_seq, n_kv;
+  const float* rope;  // [max_pos][hd/2][2] (cos, sin), or null
+};
+
+}  // namespace lsd

@@ -1,0 +1,144 @@
+// Embedding gather and (residual-combine +) LayerNorm / RMSNorm.
+//
+// K1-K3 of SURVEY.md §2.5: wte[ids] + wpe[pos] (`server.py:79-83`; dropout is a
+// no-op in eval).  K4: LayerNorm eps 1e-5 ([tf5.15] modeling_gpt2.py:252-254,
+// `server.py:101`), RMSNorm for Llama.
+//
+// The norm kernel is also the split-K reduction point: a residual GEMM that
+// split K across workgroups leaves fp32 slabs [S][T][H]; this kernel computes
+//   x[t] += bias + sum_s slab[s][t]       (written back, fp32 residual stream)
+//   y[t]  = norm(x[t]) * w (+ b)          (bf16, the next GEMM's A operand)
+// in one pass over the row -- the "combine in the next kernel's prologue"
+// launch-boundary reduce (guide §5 Projection GEMM item 2), deterministic.
+#include "common.h"
+
+namespace lsd {
+
+// One block per token row; each thread moves 8 contiguous elements per step.
+__global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids,
+                                                    const int* __restrict__ pos,
+                                                    const bf16* __restrict__ wte,
+                                                    const bf16* __restrict__ wpe, float* out,
+                                                    int H, int vocab) {
+  const int t = blockIdx.x;
+  int id = ids[t];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);  // never read out of bounds
+  const bf16* e = wte + (long)id * H;
+  const bf16* pe = wpe ? wpe + (long)pos[t] * H : nullptr;
+  float* o = out + (long)t * H;
+  for (int c = threadIdx.x * 8; c < H; c += blockDim.x * 8) {
+    bf16x8 a = ld8(e + c);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+    if (pe) {
+      bf16x8 b = ld8(pe + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += bf2f(b[j]);
+    }
+    *reinterpret_cast<f32x4*>(o + c) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(o + c + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+// Row kernel: H <= 4 * 256 * MAXV floats kept in registers between passes.
+template <int MAXV, bool RMS>
+__global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __restrict__ slab,
+                                                   int splits, const bf16* __restrict__ pbias,
+                                                   const bf16* __restrict__ w,
+                                                   const bf16* __restrict__ b, bf16* out, int T,
+                                                   int H, float eps, const int* __restrict__ rows) {
+  __shared__ float red[16];
+  const int t = blockIdx.x;
+  const int src = rows ? rows[t] : t;  // optional row gather (last-token rows)
+  float* xr = x + (long)src * H;
+  f32x4 v[MAXV];
+  float s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = (threadIdx.x + i * 256) * 4;
+    if (c < H) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(xr + c);
+      if (slab) {
+        for (int s = 0; s < splits; ++s)
+          a += *reinterpret_cast<const f32x4*>(slab + ((long)s * T + src) * H + c);
+        if (pbias) {
+          bf16x4 pb = ld4(pbias + c);
+          a += f32x4{bf2f(pb[0]), bf2f(pb[1]), bf2f(pb[2]), bf2f(pb[3])};
+        }
+        *reinterpret_cast<f32x4*>(xr + c) = a;
+      }
+      v[i] = a;
+      if (!RMS) s1 += a[0] + a[1] + a[2] + a[3];
+    } else {
+      v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if (out == nullptr) return;  // combine-only (flush)
+  float mean = 0.f;
+  if (!RMS) mean = block_sum(s1, red) / H;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = (threadIdx.x + i * 256) * 4;
+    if (c < H) {
+      f32x4 d = v[i] - mean;
+      s2 += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    }
+  }
+  const float rstd = rsqrtf(block_sum(s2, red) / H + eps);
+  bf16* o = out + (long)t * H;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = (threadIdx.x + i * 256) * 4;
+    if (c < H) {
+      bf16x4 ww = ld4(w + c);
+      f32x4 y = (v[i] - mean) * rstd;
+      bf16x4 r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float z = y[j] * bf2f(ww[j]);
+        if (!RMS) z += bf2f(b[c + j]);
+        r[j] = f2bf(z);
+      }
+      st4(o + c, r);
+    }
+  }
+}
+
+}  // namespace lsd
+
+using namespace lsd;
+
+extern "C" hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte, const bf16* wpe,
+                                float* out, int T, int H, int vocab, hipStream_t st) {
+  if (T == 0) return hipSuccess;
+  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, st, ids, pos, wte, wpe, out, H, vocab);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t lsd_norm(float* x, const float* slab, int splits, const bf16* pbias,
+                               const bf16* w, const bf16* b, bf16* out, int T, int H, float eps,
+                               int rms, const int* rows, int nrows, hipStream_t st) {
+  const int n = rows ? nrows : T;
+  if (n == 0) return hipSuccess;
+  const int maxv = (H + 1023) / 1024;
+#define LSD_NORM(MV)                                                                          \
+  if (rms)                                                                                    \
+    hipLaunchKernelGGL((norm_kernel<MV, true>), dim3(n), dim3(256), 0, st, x, slab, splits,  \
+                       pbias, w, b, out, T, H, eps, rows);                                    \
+  else                                                                                        \
+    hipLaunchKernelGGL((norm_kernel<MV, false>), dim3(n), dim3(256), 0, st, x, slab, splits, \
+                       pbias, w, b, out, T, H, eps, rows);
+  if (maxv <= 2) {
+    LSD_NORM(2)
+  } else if (maxv <= 4) {
+    LSD_NORM(4)
+  } else if (maxv <= 8) {
+    LSD_NORM(8)
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef LSD_NORM
+  return hipGetLastError();
+}

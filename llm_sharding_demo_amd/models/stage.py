@@ -99,12 +99,11 @@ class StageModel:
 
     def head(self, x: torch.Tensor, meta: BatchMeta, all_logits: bool = False) -> torch.Tensor:
         be, c = self.backend, self.cfg
-        if not all_logits and not meta.is_decode:
-            x = be.gather_rows(x, meta.last_idx)
+        rows = None if (all_logits or meta.is_decode) else meta.last_idx  # last query per sequence
         if c.arch == "gpt2":
-            xn = be.norm_rows(x, self.w["ln_f.weight"], self.w["ln_f.bias"], c.norm_eps, rms=False)
-            return be.logits(xn, self.lm_head_weight)
-        xn = be.norm_rows(x, self.w["norm.weight"], None, c.norm_eps, rms=True)
+            xn = be.norm_rows(x, self.w["ln_f.weight"], self.w["ln_f.bias"], c.norm_eps, False, rows)
+        else:
+            xn = be.norm_rows(x, self.w["norm.weight"], None, c.norm_eps, True, rows)
         return be.logits(xn, self.lm_head_weight)
 
     @property

@@ -65,7 +65,9 @@ class ReferenceBackend(Backend):
         self._combine(r)
         return ref.rmsnorm(r.x, w, eps)
 
-    def norm_rows(self, x, w, b, eps, rms: bool):
+    def norm_rows(self, x, w, b, eps, rms: bool, rows=None):
+        if rows is not None:
+            x = x.index_select(0, rows.long())
         return ref.rmsnorm(x, w, eps) if rms else ref.layernorm(x, w, b, eps)
 
     def qkv_kv_append(self, xn, w, b, cache_k, cache_v, meta, mcfg):

@@ -1,0 +1,194 @@
+"""HIP backend: the engine ops on the hand-written gfx950 kernels (_C.so).
+
+There is no fallback: constructing `HipBackend` without the built extension
+raises, so a GPU run can never silently execute eager PyTorch math.
+
+Device weight layout (set up once per stage by `prepare_stage`):
+  * lm_head rows padded to a multiple of 64 (50257 -> 50304) so the logits
+    GEMM tiles evenly; padded logits are never sampled (sampler scans < V).
+  * Llama q/k projection rows re-ordered per head so RoPE pairs (i, i+hd/2)
+    become adjacent columns (2i, 2i+1): the QKV epilogue then rotates with one
+    lane exchange.  Q.K is invariant to a common permutation of head dims, so
+    q and the K cache simply live in that order.
+  * Llama gate/up rows interleaved in 16-row blocks so one wave holds the gate
+    and up value of the same output column (silu(gate)*up fused epilogue).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import Backend, Residual
+
+_C = None
+_ERR: Optional[BaseException] = None
+
+
+def _load():
+    global _C, _ERR
+    if _C is not None:
+        return _C
+    try:
+        from .. import _C as ext  # built in-tree by ops/build.py
+    except ImportError as e:  # pragma: no cover
+        _ERR = e
+        raise RuntimeError(
+            "llm_sharding_demo_amd._C (the gfx950 HIP kernels) is not built or failed to load; "
+            "run `python -m llm_sharding_demo_amd.ops.build` (or __graft_entry__.build())") from e
+    _C = ext
+    return _C
+
+
+def extension_loaded() -> bool:
+    try:
+        _load()
+        return True
+    except Exception:
+        return False
+
+
+def rope_pair_permutation(n_heads: int, hd: int) -> torch.Tensor:
+    half = hd // 2
+    per = []
+    for i in range(half):
+        per += [i, i + half]
+    idx = torch.tensor(per)
+    return torch.cat([h * hd + idx for h in range(n_heads)])
+
+
+def interleave_gate_up(w: torch.Tensor, f: int, blk: int = 16) -> torch.Tensor:
+    gate, up = w[:f], w[f:]
+    h = w.shape[1]
+    return torch.stack([gate.reshape(f // blk, blk, h), up.reshape(f // blk, blk, h)], 1).reshape(2 * f, h)
+
+
+def rope_table(max_pos: int, hd: int, theta: float, device) -> torch.Tensor:
+    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
+    ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.stack([ang.cos(), ang.sin()], -1).float().contiguous().to(device)
+
+
+def prefill_tiles(meta) -> torch.Tensor:
+    """(sequence, query offset) of every 64-query tile of a packed batch."""
+    qlens = meta.host_qlens
+    tiles = [(i, off) for i, n in enumerate(qlens) for off in range(0, n, 64)]
+    return torch.tensor(tiles, dtype=torch.int32).reshape(-1, 2)
+
+
+class HipBackend(Backend):
+    name = "hip"
+    TARGET_BLOCKS = 512  # >> 256 CUs so every CU streams
+
+    def __init__(self):
+        self.C = _load()
+
+    # ------------------------------------------------------------------
+    def prepare_stage(self, stage) -> None:
+        cfg, w, dev = stage.cfg, stage.w, stage.device
+        if stage.last:
+            head = w["wte"] if cfg.arch == "gpt2" else w["lm_head"]
+            pad = torch.zeros(cfg.vocab_padded, cfg.hidden, dtype=head.dtype, device=dev)
+            pad[: cfg.vocab_size] = head
+            stage._lm_head_padded = pad
+        if cfg.arch == "llama":
+            perm_q = rope_pair_permutation(cfg.n_heads, cfg.head_dim)
+            perm_k = rope_pair_permutation(cfg.n_kv_heads, cfg.head_dim) + cfg.q_size
+            keep = torch.arange(cfg.q_size + cfg.kv_size, cfg.qkv_size)
+            perm = torch.cat([perm_q, perm_k, keep]).to(dev)
+            for i in stage.layers:
+                p = f"layers.{i}."
+                w[p + "self_attn.qkv.weight"] = w[p + "self_attn.qkv.weight"].index_select(0, perm).contiguous()
+                w[p + "mlp.gate_up.weight"] = interleave_gate_up(w[p + "mlp.gate_up.weight"], cfg.ffn).contiguous()
+            stage._rope = rope_table(stage.max_seq, cfg.head_dim, cfg.rope_theta, dev)
+        else:
+            stage._rope = None
+        self._rope = getattr(stage, "_rope", None)
+        stage._hip_prepared = True
+
+    # ------------------------------------------------------------------
+    @staticmethod
+    def _tiled(M: int) -> bool:
+        return M > 64
+
+    def _resid_splits(self, M: int, N: int, K: int) -> int:
+        if self._tiled(M):
+            tiles = math.ceil(M / 128) * math.ceil(N / 128)
+            return max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
+        blocks = N // 16
+        return max(1, min(math.ceil(self.TARGET_BLOCKS / blocks), K // 32 // 8 or 1))
+
+    # ------------------------------------------------------------------
+    def embed(self, ids, pos, wte, wpe):
+        return self.C.embed(ids, pos, wte, wpe)
+
+    def _norm(self, r: Residual, w, b, eps, rms: bool):
+        self._flush_extra(r)
+        slab, pb = (r.pending[0] if r.pending else (None, None))
+        out = self.C.norm(r.x, slab, pb, w, b, eps, rms, None, True)
+        r.pending.clear()
+        return out
+
+    def _flush_extra(self, r: Residual) -> None:
+        while len(r.pending) > 1:
+            slab, pb = r.pending.pop(0)
+            self.C.norm(r.x, slab, pb, None, None, 0.0, True, None, False)
+
+    def flush(self, r: Residual):
+        for slab, pb in r.pending:
+            self.C.norm(r.x, slab, pb, None, None, 0.0, True, None, False)
+        r.pending.clear()
+        return r.x
+
+    def layernorm(self, r, w, b, eps):
+        return self._norm(r, w, b, eps, False)
+
+    def rmsnorm(self, r, w, eps):
+        return self._norm(r, w, None, eps, True)
+
+    def norm_rows(self, x, w, b, eps, rms: bool, rows=None):
+        return self.C.norm(x, None, None, w, b, eps, rms, rows, True)
+
+    def qkv_kv_append(self, xn, w, b, cache_k, cache_v, meta, mcfg):
+        return self.C.linear_qkv(xn, w, b, cache_k, cache_v, meta.token_slots, meta.token_pos,
+                                 mcfg.q_size, mcfg.kv_size, mcfg.head_dim, self._rope,
+                                 self._tiled(xn.shape[0]))
+
+    def attention(self, q, cache_k, cache_v, meta):
+        n_kv, hd = cache_k.shape[1], cache_k.shape[3]
+        nh = q.shape[1] // hd
+        if meta.is_decode:
+            B = meta.num_seqs
+            splits = 1
+            if B * n_kv < self.TARGET_BLOCKS:
+                splits = min(math.ceil(self.TARGET_BLOCKS / (B * n_kv)), max(1, math.ceil(meta.max_ctx / 256)))
+            return self.C.attn_decode(q, cache_k, cache_v, meta.seq_slots, meta.token_pos, nh, splits)
+        tiles = getattr(meta, "_tiles", None)
+        if tiles is None:
+            tiles = prefill_tiles(meta).to(q.device)
+            meta._tiles = tiles
+        return self.C.attn_prefill(q, cache_k, cache_v, tiles, meta.seq_slots, meta.q_start,
+                                   meta.cu_q, nh)
+
+    def linear(self, a, w, b=None, act: str = "none"):
+        code = {"none": 0, "gelu": 1, "silu_mul": 2}[act]
+        return self.C.linear(a, w, b, code, self._tiled(a.shape[0]))
+
+    def linear_residual(self, a, w, b, r: Residual) -> None:
+        M, K = a.shape
+        N = w.shape[0]
+        splits = self._resid_splits(M, N, K)
+        slab = self.C.linear_residual(a, w, b, r.x, splits, self._tiled(M))
+        if slab is not None:
+            r.pending.append((slab, b))
+
+    def logits(self, xn, w):
+        return self.C.linear_f32(xn, w, self._tiled(xn.shape[0]))
+
+    def sample(self, logits, samp, vocab: int):
+        return self.C.sample(logits, vocab, samp.temperature, samp.top_k, samp.greedy,
+                             samp.seeds, samp.step)
+
+    def gather_rows(self, x, idx):
+        return x.index_select(0, idx.long())

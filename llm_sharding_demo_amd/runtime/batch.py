@@ -33,6 +33,7 @@ class BatchMeta:
     max_q: int
     max_ctx: int  # upper bound on q_start + qlen (host-side, for grid sizing)
     is_decode: bool
+    host_qlens: Optional[List[int]] = None  # per-sequence query counts (host copy)
 
     @staticmethod
     def build(slots: Sequence[int], starts: Sequence[int], qlens: Sequence[int],
@@ -57,7 +58,7 @@ class BatchMeta:
             last_idx=torch.tensor([c - 1 for c in cu[1:]], **i32),
             num_tokens=T, num_seqs=B, max_q=max(qlens, default=0),
             max_ctx=max_ctx if max_ctx is not None else mc,
-            is_decode=all(n == 1 for n in qlens))
+            is_decode=all(n == 1 for n in qlens), host_qlens=list(qlens))
 
     @staticmethod
     def decode(slots: Sequence[int], positions: Sequence[int], device,
@@ -71,7 +72,7 @@ class BatchMeta:
         ar = torch.arange(B + 1, **i32)
         return BatchMeta(token_slots=sl, token_pos=pos, seq_slots=sl, q_start=pos,
                          cu_q=ar, last_idx=ar[:B], num_tokens=B, num_seqs=B, max_q=1,
-                         max_ctx=max_ctx, is_decode=True)
+                         max_ctx=max_ctx, is_decode=True, host_qlens=[1] * B)
 
     def advance(self) -> None:
         """Decode only: every sequence moves one position forward (in place)."""

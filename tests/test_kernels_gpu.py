@@ -1,0 +1,206 @@
+"""HIP kernel numerics on an MI355X, each vs a plain PyTorch fp32 reference
+(ops/reference.py) of the same op.  bf16 inputs, fp32 accumulation.
+"""
+import math
+
+import pytest
+import torch
+
+from llm_sharding_demo_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def C():
+    from llm_sharding_demo_amd.ops.hip import _load
+
+    return _load()
+
+
+def bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=DEV) * scale).to(torch.bfloat16)
+
+
+def close(a, b, atol, rtol=2e-2):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
+
+
+def test_embed(C):
+    V, H, P, T = 1000, 256, 64, 37
+    wte, wpe = bf(V, H, seed=1), bf(P, H, seed=2)
+    ids = torch.randint(0, V, (T,), dtype=torch.int32, device=DEV)
+    pos = torch.randint(0, P, (T,), dtype=torch.int32, device=DEV)
+    close(C.embed(ids, pos, wte, wpe), ref.embed(ids, pos, wte, wpe), 1e-6)
+    close(C.embed(ids, pos, wte, None), ref.embed(ids, pos, wte, None), 1e-6)
+
+
+@pytest.mark.parametrize("H", [128, 768, 1600, 4096])
+@pytest.mark.parametrize("rms", [False, True])
+def test_norm_with_slab_combine(C, H, rms):
+    T, S = 19, 3
+    x = torch.randn(T, H, device=DEV)
+    slab = torch.randn(S, T, H, device=DEV) * 0.1
+    pb = bf(H, scale=0.1, seed=3)
+    w, b = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16(), bf(H, scale=0.1, seed=4)
+    x_ref = x + slab.sum(0) + pb.float()
+    y_ref = ref.rmsnorm(x_ref, w, 1e-5) if rms else ref.layernorm(x_ref, w, b, 1e-5)
+    y = C.norm(x, slab, pb, w, None if rms else b, 1e-5, rms, None, True)
+    close(x, x_ref, 1e-5)
+    close(y, y_ref, 2e-2)
+    rows = torch.tensor([3, 0, 18], dtype=torch.int32, device=DEV)
+    y2 = C.norm(x, None, None, w, None if rms else b, 1e-5, rms, rows, True)
+    close(y2, y_ref[rows.long()], 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 65, 200])
+@pytest.mark.parametrize("act", ["none", "gelu", "silu_mul"])
+def test_linear(C, M, act):
+    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
+
+    N, K = 384, 640
+    a, w, bias = bf(M, K, seed=5), bf(N, K, scale=0.05, seed=6), bf(N, scale=0.1, seed=7)
+    tiled = M > 64
+    if act == "silu_mul":
+        y = C.linear(a, interleave_gate_up(w, N // 2).contiguous(), None, 2, tiled)
+        y_ref = ref.silu_mul(*ref.linear(a, w).split(N // 2, 1))
+    else:
+        y = C.linear(a, w, bias, 1 if act == "gelu" else 0, tiled)
+        y_ref = ref.linear(a, w, bias)
+        if act == "gelu":
+            y_ref = ref.gelu_new(y_ref)
+    close(y, y_ref, 3e-2)
+
+
+@pytest.mark.parametrize("M,splits", [(3, 1), (16, 4), (64, 5), (100, 1), (130, 3)])
+def test_linear_residual_and_f32(C, M, splits):
+    N, K = 256, 1024
+    a, w, bias = bf(M, K, seed=8), bf(N, K, scale=0.05, seed=9), bf(N, scale=0.1, seed=10)
+    tiled = M > 64
+    x = torch.randn(M, N, device=DEV)
+    x_ref = x + ref.linear(a, w, bias)
+    slab = C.linear_residual(a, w, bias, x, splits, tiled)
+    if slab is not None:
+        C.norm(x, slab, bias, None, None, 0.0, True, None, False)
+    close(x, x_ref, 2e-3, 1e-3)
+    close(C.linear_f32(a, w, tiled), ref.linear(a, w), 2e-3, 1e-3)
+
+
+def test_gemm_large_prefill_shape(C):
+    M, N, K = 1000, 4800, 1600
+    a, w = bf(M, K, seed=11), bf(N, K, scale=0.03, seed=12)
+    close(C.linear(a, w, None, 0, True), ref.linear(a, w), 3e-2)
+
+
+def _cache(slots, n_kv, S, hd):
+    return (torch.zeros(slots, n_kv, S, hd, dtype=torch.bfloat16, device=DEV),
+            torch.zeros(slots, n_kv, S, hd, dtype=torch.bfloat16, device=DEV))
+
+
+@pytest.mark.parametrize("rope", [False, True])
+def test_qkv_kv_append(C, rope):
+    from llm_sharding_demo_amd.ops.hip import rope_pair_permutation, rope_table
+
+    nh, n_kv, hd, H = 4, 2, 64, 256
+    qs, kvs = nh * hd, n_kv * hd
+    T, slots, S = 10, 3, 32
+    a, w, bias = bf(T, H, seed=13), bf(qs + 2 * kvs, H, scale=0.05, seed=14), bf(qs + 2 * kvs, scale=0.1, seed=15)
+    tslot = torch.tensor([0] * 4 + [2] * 6, dtype=torch.int32, device=DEV)
+    tpos = torch.tensor(list(range(4)) + list(range(5, 11)), dtype=torch.int32, device=DEV)
+    kc, vc = _cache(slots, n_kv, S, hd)
+    kr, vr = _cache(slots, n_kv, S, hd)
+    y = ref.linear(a, w, bias)
+    q_ref = y[:, :qs].reshape(T, nh, hd)
+    k_ref = y[:, qs:qs + kvs].reshape(T, n_kv, hd)
+    v_ref = y[:, qs + kvs:].reshape(T, n_kv, hd)
+    if rope:
+        q_ref = ref.apply_rope(q_ref, tpos.cpu(), 10000.0)
+        k_ref = ref.apply_rope(k_ref, tpos.cpu(), 10000.0)
+        perm = torch.cat([rope_pair_permutation(nh, hd), rope_pair_permutation(n_kv, hd) + qs,
+                          torch.arange(qs + kvs, qs + 2 * kvs)]).to(DEV)
+        w, bias = w[perm].contiguous(), bias[perm].contiguous()
+        table = rope_table(S, hd, 10000.0, DEV)
+        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, table, False)
+        # un-permute the pair-interleaved head dims for comparison
+        p1 = rope_pair_permutation(1, hd)
+        inv = torch.argsort(p1).to(DEV)
+        q = q.reshape(T, nh, hd)[:, :, inv]
+        kc = kc[..., inv]
+    else:
+        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, None, False).reshape(T, nh, hd)
+    ref.kv_append(kr, vr, k_ref, v_ref, tslot, tpos)
+    close(q, q_ref, 3e-2)
+    close(kc, kr, 3e-2)
+    close(vc, vr, 3e-2)
+
+
+@pytest.mark.parametrize("hd,nh,n_kv", [(64, 4, 4), (64, 8, 2), (128, 8, 2), (128, 32, 8)])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_attention_decode(C, hd, nh, n_kv, splits):
+    B, slots, S = 5, 6, 300
+    kc, vc = bf(slots, n_kv, S, hd, seed=16), bf(slots, n_kv, S, hd, seed=17)
+    q = bf(B, nh * hd, seed=18)
+    seq_slots = torch.tensor([5, 0, 2, 3, 1], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([0, 17, 63, 140, 299], dtype=torch.int32, device=DEV)
+    o = C.attn_decode(q, kc, vc, seq_slots, pos, nh, splits)
+    cu = torch.arange(B + 1, dtype=torch.int32)
+    o_ref = ref.attention(q.reshape(B, nh, hd).cpu(), kc.cpu(), vc.cpu(), seq_slots.cpu(), pos.cpu(), cu)
+    close(o.reshape(B, nh, hd), o_ref, 2e-2)
+
+
+@pytest.mark.parametrize("hd,nh,n_kv", [(64, 4, 4), (128, 8, 2)])
+def test_attention_prefill_ragged_chunked(C, hd, nh, n_kv):
+    from llm_sharding_demo_amd.ops.hip import prefill_tiles
+    from llm_sharding_demo_amd.runtime.batch import BatchMeta
+
+    slots, S = 4, 400
+    kc, vc = bf(slots, n_kv, S, hd, seed=19), bf(slots, n_kv, S, hd, seed=20)
+    # seq 0: fresh 130 tokens; seq 1: 1 token; seq 2: chunk of 70 after 200 cached; seq 3: 64
+    meta = BatchMeta.build([1, 0, 3, 2], [0, 0, 200, 5], [130, 1, 70, 64], DEV)
+    q = bf(meta.num_tokens, nh * hd, seed=21)
+    o = C.attn_prefill(q, kc, vc, prefill_tiles(meta).to(DEV), meta.seq_slots, meta.q_start,
+                       meta.cu_q, nh)
+    o_ref = ref.attention(q.reshape(-1, nh, hd).cpu(), kc.cpu(), vc.cpu(), meta.seq_slots.cpu(),
+                          meta.q_start.cpu(), meta.cu_q.cpu())
+    close(o.reshape(-1, nh, hd), o_ref, 2e-2)
+
+
+def test_attention_prefill_large_logits_stable(C):
+    """Spiky scores force the online-softmax rescale path (guide rule 26)."""
+    from llm_sharding_demo_amd.ops.hip import prefill_tiles
+    from llm_sharding_demo_amd.runtime.batch import BatchMeta
+
+    hd, nh = 64, 2
+    kc, vc = bf(1, nh, 256, hd, scale=3.0, seed=22), bf(1, nh, 256, hd, seed=23)
+    kc[0, :, 200] *= 8  # one late key dominates
+    meta = BatchMeta.build([0], [0], [256], DEV)
+    q = bf(256, nh * hd, scale=3.0, seed=24)
+    o = C.attn_prefill(q, kc, vc, prefill_tiles(meta).to(DEV), meta.seq_slots, meta.q_start,
+                       meta.cu_q, nh)
+    o_ref = ref.attention(q.reshape(-1, nh, hd).cpu(), kc.cpu(), vc.cpu(), meta.seq_slots.cpu(),
+                          meta.q_start.cpu(), meta.cu_q.cpu())
+    assert torch.isfinite(o.float()).all()
+    close(o.reshape(-1, nh, hd), o_ref, 3e-2)
+
+
+def test_sampler(C):
+    from llm_sharding_demo_amd.runtime.batch import counter_uniform
+
+    B, V, Vp = 6, 50257, 50304
+    logits = torch.randn(B, Vp, device=DEV) * 3
+    logits[:, V:] = 100.0  # padding must never be selected
+    temp = torch.tensor([1.0, 0.6, 0.6, 2.0, 1.0, 0.6], device=DEV)
+    topk = torch.tensor([1, 40, 40, 5, 1024, 40], dtype=torch.int32, device=DEV)
+    greedy = torch.tensor([1, 0, 0, 0, 0, 1], dtype=torch.int32, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 7919
+    step = torch.full((B,), 3, dtype=torch.int64, device=DEV)
+    out = C.sample(logits, V, temp, topk, greedy, seeds, step)
+    exp = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), greedy.cpu(),
+                     counter_uniform(seeds.cpu(), step.cpu()), V)
+    assert out.cpu().tolist() == exp.tolist()
+    for r in range(B):
+        k = 1 if greedy[r] else int(topk[r])
+        assert int(out[r]) in set(torch.topk(logits[r, :V], k).indices.tolist())
