@@ -16,7 +16,7 @@ typedef lsd_bf16_t bf16;
 using lsd::GemmParams;
 
 extern "C" {
-hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, hipStream_t st);
+hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws, hipStream_t st);
 hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte, const bf16* wpe, float* out,
                      int T, int H, int vocab, hipStream_t st);
 hipError_t lsd_norm(float* x, const float* slab, int splits, const bf16* pbias, const bf16* w,
@@ -51,6 +51,14 @@ void need(const torch::Tensor& t, c10::ScalarType dt, const char* name) {
   TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
 }
 
+long long* g_stamps = nullptr;  // diagnostic phase stamps (tools/microbench.py "stamps")
+
+void set_stamps(c10::optional<torch::Tensor> t) {
+  if (!t.has_value()) { g_stamps = nullptr; return; }
+  need(*t, torch::kInt64, "stamps");
+  g_stamps = reinterpret_cast<long long*>(t->data_ptr<int64_t>());
+}
+
 void need_rows(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with unit last stride");
   TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8 elements");
@@ -82,21 +90,50 @@ GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, bool tile
   if (tiled) {
     TORCH_CHECK(p.K % 64 == 0, "tiled GEMM needs K % 64 == 0, got ", p.K);
   } else {
-    TORCH_CHECK(p.M >= 1 && p.M <= 64, "skinny GEMM needs 1 <= M <= 64, got ", p.M);
-    TORCH_CHECK(p.K % 32 == 0, "skinny GEMM needs K % 32 == 0, got ", p.K);
+    TORCH_CHECK(p.M >= 1 && p.M <= 64, "decode GEMM needs 1 <= M <= 64, got ", p.M);
+    TORCH_CHECK(p.K % 32 == 0, "decode GEMM needs K % 32 == 0, got ", p.K);
+    TORCH_CHECK(p.N % 64 == 0, "decode GEMM needs N % 64 == 0 (pad the weight), got ", p.N);
   }
   return p;
 }
 
-int check_splits(int splits, const GemmParams& p, bool tiled) {
+// Launch with split-K bookkeeping: the decode path needs persistent zeroed
+// ticket counters (one per column tile) and an fp32 partial-tile workspace.
+void run_gemm(GemmParams& p, int epi, bool tiled, int64_t splits,
+              const c10::optional<torch::Tensor>& counters, const torch::Tensor& like,
+              const char* what) {
   const int kt = tiled ? p.K / 64 : p.K / 32;
-  TORCH_CHECK(splits >= 1 && splits <= kt, "splits must be in [1, ", kt, "], got ", splits);
-  return splits;
+  TORCH_CHECK(splits >= 1 && splits <= kt, what, ": splits must be in [1, ", kt, "], got ", splits);
+  p.splits = (int)splits;
+  int* cnt = nullptr;
+  float* ws = nullptr;
+  torch::Tensor wsbuf;
+  if (!tiled) {
+    const int nw = epi == EPI_SILU_MUL ? 2 : 1;
+    TORCH_CHECK(p.N % (64 * nw) == 0, what, ": N must be a multiple of ", 64 * nw);
+    const long tiles = p.N / (64 * nw);
+    if (splits > 1) {
+      TORCH_CHECK(counters.has_value(), what, ": split-K needs the ticket counter buffer");
+      need(*counters, torch::kInt32, "counters");
+      TORCH_CHECK(counters->is_contiguous() && counters->numel() >= tiles,
+                  what, ": counter buffer too small (", counters->numel(), " < ", tiles, ")");
+      cnt = counters->data_ptr<int>();
+      const long rows = ((p.M + 15) / 16) * 16;
+      const long bytes = tiles * splits * rows * 64 * nw * 4;
+      TORCH_CHECK(splits * rows * 64 * nw * 4 < (1L << 31), what, ": split workspace too large");
+      wsbuf = torch::empty({bytes / 4}, like.options().dtype(torch::kFloat32));
+      ws = wsbuf.data_ptr<float>();
+    }
+  }
+  p.stamps = g_stamps;
+  check_hip(lsd_gemm(&p, epi, tiled ? 1 : 0, cnt, ws, cur_stream()), what);
 }
+
 
 // out = act(a @ w^T + bias), bf16
 torch::Tensor linear(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,
-                     int64_t act, bool tiled) {
+                     int64_t act, bool tiled, int64_t splits,
+                     c10::optional<torch::Tensor> counters) {
   GemmParams p = base_params(a, w, tiled);
   p.bias = opt_bias(bias, p.N);
   int epi = act == 1 ? EPI_GELU : (act == 2 ? EPI_SILU_MUL : EPI_BF16);
@@ -105,48 +142,52 @@ torch::Tensor linear(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tens
   auto out = torch::empty({p.M, n_out}, a.options());
   if (p.M == 0) return out;
   p.out = out.data_ptr(); p.ldo = n_out;
-  check_hip(lsd_gemm(&p, epi, tiled, cur_stream()), "linear");
+  run_gemm(p, epi, tiled, splits, counters, a, "linear");
   return out;
 }
 
 // fp32 logits = a @ w^T
-torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, bool tiled) {
+torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, bool tiled, int64_t splits,
+                         c10::optional<torch::Tensor> counters) {
   GemmParams p = base_params(a, w, tiled);
   auto out = torch::empty({p.M, p.N}, a.options().dtype(torch::kFloat32));
   if (p.M == 0) return out;
   p.out = out.data_ptr(); p.ldo = p.N;
-  check_hip(lsd_gemm(&p, EPI_F32, tiled, cur_stream()), "linear_f32");
+  run_gemm(p, EPI_F32, tiled, splits, counters, a, "linear_f32");
   return out;
 }
 
-// x += a @ w^T + bias (splits == 1) or return fp32 slabs [splits, M, N] to be
-// folded in by the next norm (splits > 1).
+// x += a @ w^T + bias.  Decode path: any split, combined in-kernel.  Tiled
+// path with splits > 1: returns fp32 slabs [splits, M, N] that the next norm
+// folds in.
 c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
                                               c10::optional<torch::Tensor> bias, torch::Tensor x,
-                                              int64_t splits, bool tiled) {
+                                              int64_t splits, bool tiled,
+                                              c10::optional<torch::Tensor> counters) {
   GemmParams p = base_params(a, w, tiled);
   need(x, torch::kFloat32, "x");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(0) == p.M && x.size(1) == p.N,
               "residual x must be contiguous [M, N]");
-  p.splits = check_splits(splits, p, tiled);
   if (p.M == 0) return c10::nullopt;
-  if (p.splits == 1) {
-    p.bias = opt_bias(bias, p.N);
-    p.out = x.data_ptr(); p.ldo = p.N;
-    check_hip(lsd_gemm(&p, EPI_RESID, tiled, cur_stream()), "linear_residual");
-    return c10::nullopt;
+  if (tiled && splits > 1) {
+    TORCH_CHECK(splits <= p.K / 64, "splits must be <= K/64");
+    auto slab = torch::empty({splits, p.M, p.N}, x.options());
+    p.slab = slab.data_ptr<float>();
+    run_gemm(p, EPI_SLAB, true, splits, c10::nullopt, x, "linear_residual(split)");
+    return slab;
   }
-  auto slab = torch::empty({p.splits, p.M, p.N}, x.options());
-  p.slab = slab.data_ptr<float>();
-  check_hip(lsd_gemm(&p, EPI_SLAB, tiled, cur_stream()), "linear_residual(split)");
-  return slab;
+  p.bias = opt_bias(bias, p.N);
+  p.out = x.data_ptr(); p.ldo = p.N;
+  run_gemm(p, EPI_RESID, tiled, splits, counters, x, "linear_residual");
+  return c10::nullopt;
 }
 
 // QKV projection: returns q bf16 [M, q_size]; k, v written into the caches.
 torch::Tensor linear_qkv(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,
                          torch::Tensor kc, torch::Tensor vc, torch::Tensor tslot,
                          torch::Tensor tpos, int64_t q_size, int64_t kv_size, int64_t hd,
-                         c10::optional<torch::Tensor> rope, bool tiled) {
+                         c10::optional<torch::Tensor> rope, bool tiled, int64_t splits,
+                         c10::optional<torch::Tensor> counters) {
   GemmParams p = base_params(a, w, tiled);
   p.bias = opt_bias(bias, p.N);
   need(kc, torch::kBFloat16, "k_cache");
@@ -173,7 +214,7 @@ torch::Tensor linear_qkv(torch::Tensor a, torch::Tensor w, c10::optional<torch::
   auto q = torch::empty({p.M, q_size}, a.options());
   if (p.M == 0) return q;
   p.out = q.data_ptr(); p.ldo = q_size;
-  check_hip(lsd_gemm(&p, EPI_QKV, tiled, cur_stream()), "linear_qkv");
+  run_gemm(p, EPI_QKV, tiled, splits, counters, a, "linear_qkv");
   return q;
 }
 
@@ -318,6 +359,8 @@ torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch:
                      torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step) {
   need(logits, torch::kFloat32, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && V <= logits.size(1) && V >= 1, "logits [B, >=V]");
+  TORCH_CHECK(logits.stride(0) % 4 == 0 && logits.size(1) % 4 == 0, "logits row length must be a multiple of 4");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0, "logits must be 16-byte aligned");
   const int B = logits.size(0);
   need(temp, torch::kFloat32, "temperature");
   need(topk, torch::kInt32, "top_k");
@@ -348,5 +391,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_decode", &attn_decode);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample);
+  m.def("set_stamps", &set_stamps);
   m.attr("arch") = "gfx950";
 }

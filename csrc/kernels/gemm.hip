@@ -6,11 +6,11 @@
 // 16x16x32 B-operand fragment is one 16-byte load.
 //
 // Two kernels:
-//  * gemm_skinny  -- M <= 64 (decode microbatches).  Weight-bandwidth bound:
-//    W is streamed HBM -> VGPRs with 16-byte loads, no LDS round trip (guide
-//    §5 "GEMV / M <= 16 decode weights"), the block's 4 waves split K and
-//    reduce through LDS, optional cross-workgroup split-K writes fp32 slabs
-//    that the next norm kernel folds in (no atomics, deterministic).
+//  * gemm_sk      -- M <= 64 (decode microbatches).  Weight-bandwidth bound:
+//    W streamed HBM -> VGPRs (read once, no LDS round trip), the small A
+//    operand staged through LDS with full-line LDS-DMA, split-K across
+//    workgroups for occupancy with an in-kernel last-arriver combine that
+//    runs the fused epilogue (deterministic: fixed summation order).
 //  * gemm_tiled   -- M > 64 (prefill / large microbatches).  128x128x64 block
 //    tile, 4 waves of 64x64, operands staged HBM -> LDS with 16-byte
 //    global_load_lds (LDS-DMA), XOR-swizzled on the source address so the
@@ -120,26 +120,59 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int row0, int n, 
 }
 
 // ---------------------------------------------------------------------------
-// Skinny GEMM (M <= 64)
+// Decode GEMM (M <= 64): split-K across workgroups, last-arriver combine
 // ---------------------------------------------------------------------------
-// grid = (N / (16*NW), splits); block = 256 = 4 waves splitting the block's K range.
-template <int MT, int NW, int U, int EPI>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
-  const int lane = lane_id(), wk = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int nb = blockIdx.x * 16 * NW;
-  const int split = blockIdx.y;
-  const int KT = p.K >> 5;
-  const int kb = (int)((long)KT * split / p.splits), ke = (int)((long)KT * (split + 1) / p.splits);
-  const int len = ke - kb;
-  const int wb = kb + len * wk / 4, we = kb + len * (wk + 1) / 4;
+// grid = (N / (64*NW) column tiles, S k-splits); block = 4 waves, wave w owns
+// columns [16*NW*w, 16*NW*(w+1)) of the block's tile and the whole K range of
+// the split.  Per round of up to 512 k:
+//   * A[0:M, k-range] -> LDS with 16-B LDS-DMA (global_load_lds), whole 128-B
+//     lines per instruction (not 16-row fragment-shaped loads, which double
+//     TA traffic: guide §5 "x operand through LDS in full lines"), one image of
+//     256-B rows per 128-k chunk, 16-B chunks XOR-swizzled by (row & 15) so the
+//     ds_read_b128 fragment reads are conflict-free;
+//   * every W fragment of the round is issued straight to VGPRs (W is read
+//     once: no LDS round trip), so a block costs ONE memory round trip;
+//   * one barrier, then MFMAs out of LDS (A) and registers (W).
+// S > 1: each split stores its fp32 partial tile, the last arriver (agent-scope
+// release/acquire ticket, guide §5 "In-launch split-K reduction") sums the S
+// partials and runs the fused epilogue -- so any epilogue (QKV scatter + RoPE,
+// GELU, residual add) works with any split and no extra launch is needed.
+constexpr int SK_ROUND_STEPS = 16;  // 32-k MFMA steps per round (512 k)
 
-  const bf16* wp[NW];
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)g,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// Diagnostic phase stamps (100 MHz constant clock), written by thread 0 only
+// when p.stamps != null; slot 7 = XCC id.  Never on in production.
+#define LSD_STAMP(k)                                                                       \
+  if (p.stamps && threadIdx.x == 0)                                                        \
+    p.stamps[((long)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+
+template <int MT, int NW, int EPI>
+__global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restrict__ cnt,
+                                                      float* __restrict__ ws) {
+  constexpr int ROWS = MT * 16;
+  constexpr int CHUNK_BYTES = ROWS * 256;  // one [ROWS][128 k] bf16 image
+  constexpr int BNB = 64 * NW;             // block tile columns
+  __shared__ __attribute__((aligned(16))) char smem[4 * CHUNK_BYTES + 16];
+  int* s_flag = reinterpret_cast<int*>(smem + 4 * CHUNK_BYTES);
+
+  LSD_STAMP(0)
+  if (p.stamps && threadIdx.x == 0)
+    p.stamps[((long)blockIdx.y * gridDim.x + blockIdx.x) * 8 + 7] =
+        __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID[3:0]
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int tile = blockIdx.x, split = blockIdx.y, S = p.splits;
+  const int n_w = tile * BNB + w * 16 * NW;
+  const int KT = p.K >> 5;
+  const int kb = (int)((long)KT * split / S), ke = (int)((long)KT * (split + 1) / S);
+
+  const bf16* wrow[NW];
 #pragma unroll
-  for (int ns = 0; ns < NW; ++ns) wp[ns] = p.W + (long)(nb + 16 * ns + r) * p.ldw + g * 8;
-  const bf16* ap[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) ap[mt] = p.A + (long)min(mt * 16 + r, p.M - 1) * p.lda + g * 8;
+  for (int ns = 0; ns < NW; ++ns) wrow[ns] = p.W + (long)(n_w + 16 * ns + r) * p.ldw + g * 8;
 
   f32x4 acc[MT][NW];
 #pragma unroll
@@ -147,52 +180,113 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
 #pragma unroll
     for (int ns = 0; ns < NW; ++ns) acc[mt][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int s = wb;
-  for (; s + U <= we; s += U) {
-    bf16x8 wv[U][NW], av[U][MT];
+  for (int k0 = kb; k0 < ke; k0 += SK_ROUND_STEPS) {
+    const int nst = min(SK_ROUND_STEPS, ke - k0);
+    const int nch = (nst + 3) >> 2;
+    // A chunks: MT*4 wave-instructions (1 KiB = 4 rows of 256 B) per chunk
+    for (int inst = w; inst < nch * MT * 4; inst += 4) {
+      const int c = inst / (MT * 4), q = inst % (MT * 4);
+      const int row = q * 4 + (lane >> 4);
+      const int lch = (lane & 15) ^ (row & 15);
+      const int kk = min((k0 + c * 4) * 32 + lch * 8, p.K - 8);
+      glds16(p.A + (long)min(row, p.M - 1) * p.lda + kk, smem + c * CHUNK_BYTES + q * 1024);
+    }
+    bf16x8 wv[SK_ROUND_STEPS][NW];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int j = 0; j < SK_ROUND_STEPS; ++j)
+      if (j < nst)
 #pragma unroll
-      for (int ns = 0; ns < NW; ++ns) wv[u][ns] = ld8(wp[ns] + (long)(s + u) * 32);
+        for (int ns = 0; ns < NW; ++ns) wv[j][ns] = ld8(wrow[ns] + (long)(k0 + j) * 32);
+    __syncthreads();  // vmcnt(0): the A image and this wave's W fragments have landed
+    if (k0 == kb) { LSD_STAMP(1) }
+    auto step = [&](int j) {
+      const char* img = smem + (j >> 2) * CHUNK_BYTES;
+      const int lch = (j & 3) * 4 + g;
+      bf16x8 a[MT];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) av[u][mt] = ld8(ap[mt] + (long)(s + u) * 32);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int mt = 0; mt < MT; ++mt) {
+        const int row = mt * 16 + r;
+        a[mt] = *reinterpret_cast<const bf16x8*>(img + row * 256 + ((lch ^ (row & 15)) << 4));
+      }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int ns = 0; ns < NW; ++ns) acc[mt][ns] = mfma16(av[u][mt], wv[u][ns], acc[mt][ns]);
+        for (int ns = 0; ns < NW; ++ns) acc[mt][ns] = mfma16(a[mt], wv[j][ns], acc[mt][ns]);
+    };
+    if (nst == SK_ROUND_STEPS) {  // common case: no guards, the scheduler can hoist ds_reads
+#pragma unroll
+      for (int j = 0; j < SK_ROUND_STEPS; ++j) step(j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < SK_ROUND_STEPS; ++j)
+        if (j < nst) step(j);
+    }
+    __syncthreads();  // the image is rewritten by the next round
   }
-  for (; s < we; ++s) {
-    bf16x8 wv[NW], av[MT];
-#pragma unroll
-    for (int ns = 0; ns < NW; ++ns) wv[ns] = ld8(wp[ns] + (long)s * 32);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) av[mt] = ld8(ap[mt] + (long)s * 32);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int ns = 0; ns < NW; ++ns) acc[mt][ns] = mfma16(av[mt], wv[ns], acc[mt][ns]);
-  }
+  LSD_STAMP(2)
 
-  // Reduce the 4 waves' K-partials through LDS; wave 0 runs the epilogue.
-  __shared__ f32x4 red[3][MT * NW][64];
-  if (wk > 0) {
+  if (S > 1) {
+    // ---- publish this split's partial tile; the last arriver combines.
+    // Slab layout is lane-major ([wave][mt][ns][lane] x f32x4) so every lane
+    // moves 16 contiguous bytes; stores are write-through (sc1) and every
+    // reducer load is sc1, so no agent release/acquire fence is needed (guide
+    // §5 "In-launch split-K reduction", sc1 form; a buffer_wbl2 release per
+    // block cost ~5 us here).
+    constexpr int PER_BLOCK = 4 * MT * NW * 64;  // f32x4 per split tile
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        ws + (long)tile * S * PER_BLOCK * 4, (short)0, S * PER_BLOCK * 16, 0x00020000);
+    const int lane_off = ((w * MT * NW) * 64 + lane) * 16;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int ns = 0; ns < NW; ++ns) red[wk - 1][mt * NW + ns][lane] = acc[mt][ns];
+      for (int ns = 0; ns < NW; ++ns)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mt][ns]), rs,
+                                               split * PER_BLOCK * 16 + lane_off + (mt * NW + ns) * 1024,
+                                               0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int t = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_flag = (t == S - 1);
+      if (t == S - 1) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    LSD_STAMP(3)
+    if (*s_flag == 0) return;
+    // Sum ALL S partials (own included, from the slab) in fixed split order:
+    // the result must not depend on which split arrived last.
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int ns = 0; ns < NW; ++ns) acc[mt][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // Issue every slab load of a group before summing (no per-load branch:
+    // clamped index x 0/1 mask), so the reduce is one round trip per group
+    // instead of one per split.
+    constexpr int RG = (MT * NW <= 2) ? 8 : 4;
+    for (int s0 = 0; s0 < S; s0 += RG) {
+      f32x4 v[RG][MT][NW];
+#pragma unroll
+      for (int u = 0; u < RG; ++u) {
+        const int s2 = min(s0 + u, S - 1);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int ns = 0; ns < NW; ++ns)
+            v[u][mt][ns] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                           rs, s2 * PER_BLOCK * 16 + lane_off + (mt * NW + ns) * 1024, 0, 16));
+      }
+#pragma unroll
+      for (int u = 0; u < RG; ++u) {
+        const float msk = (s0 + u < S) ? 1.f : 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int ns = 0; ns < NW; ++ns) acc[mt][ns] += v[u][mt][ns] * msk;
+      }
+    }
   }
-  __syncthreads();
-  if (wk != 0) return;
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int ns = 0; ns < NW; ++ns) acc[mt][ns] += red[j][mt * NW + ns][lane];
+  LSD_STAMP(4)
 
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -200,13 +294,14 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
     if constexpr (EPI == EPI_SILU_MUL) {
 #pragma unroll
       for (int ns = 0; ns < NW; ns += 2)
-        epilogue4<EPI>(p, row0, nb + 16 * ns + r, acc[mt][ns], acc[mt][ns + 1], split);
+        epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns + 1], 0);
     } else {
 #pragma unroll
       for (int ns = 0; ns < NW; ++ns)
-        epilogue4<EPI>(p, row0, nb + 16 * ns + r, acc[mt][ns], acc[mt][ns], split);
+        epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns], 0);
     }
   }
+  LSD_STAMP(5)
 }
 
 // ---------------------------------------------------------------------------
@@ -320,22 +415,17 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles
 // Host launchers
 // ---------------------------------------------------------------------------
 template <int EPI>
-static hipError_t launch_skinny(const GemmParams& p, hipStream_t st) {
+static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
+  constexpr int NW = (EPI == EPI_SILU_MUL) ? 2 : 1;
   const int MT = (p.M + 15) / 16;
-  const int NW = (EPI == EPI_SILU_MUL) ? 2 : 1;
-  dim3 grid(p.N / (16 * NW), p.splits), block(256);
-#define LSD_SK(mt, u)                                                               \
-  hipLaunchKernelGGL((gemm_skinny_kernel<mt, (EPI == EPI_SILU_MUL ? 2 : 1), u, EPI>), grid, \
-                     block, 0, st, p)
+  dim3 grid(p.N / (64 * NW), p.splits), block(256);
   switch (MT) {
-    case 1: LSD_SK(1, 8); break;
-    case 2: LSD_SK(2, 4); break;
-    case 3: LSD_SK(3, 4); break;
-    case 4: LSD_SK(4, 4); break;
+    case 1: hipLaunchKernelGGL((gemm_sk_kernel<1, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
+    case 2: hipLaunchKernelGGL((gemm_sk_kernel<2, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
+    case 3: hipLaunchKernelGGL((gemm_sk_kernel<3, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
+    case 4: hipLaunchKernelGGL((gemm_sk_kernel<4, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
     default: return hipErrorInvalidValue;
   }
-#undef LSD_SK
-  (void)NW;
   return hipGetLastError();
 }
 
@@ -352,17 +442,19 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
 using namespace lsd;
 
 // C ABI used by csrc/bindings.cpp; shapes are validated there.
-extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, hipStream_t st) {
+extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws,
+                               hipStream_t st) {
 #define LSD_DISPATCH(E) \
-  case E: return tiled ? launch_tiled<E>(*p, st) : launch_skinny<E>(*p, st);
+  case E: return tiled ? launch_tiled<E>(*p, st) : launch_sk<E>(*p, cnt, ws, st);
   switch (epi) {
     LSD_DISPATCH(EPI_BF16)
     LSD_DISPATCH(EPI_GELU)
     LSD_DISPATCH(EPI_SILU_MUL)
     LSD_DISPATCH(EPI_F32)
     LSD_DISPATCH(EPI_RESID)
-    LSD_DISPATCH(EPI_SLAB)
     LSD_DISPATCH(EPI_QKV)
+    case EPI_SLAB:
+      return tiled ? launch_tiled<EPI_SLAB>(*p, st) : hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 #undef LSD_DISPATCH

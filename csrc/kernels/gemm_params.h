@@ -22,6 +22,7 @@ struct GemmParams {
   const int* tslot; const int* tpos;
   int q_size, kv_size, hd, max_seq, n_kv;
   const float* rope;  // [max_pos][hd/2][2] (cos, sin), or null
+  long long* stamps;  // diagnostic builds only: per-workgroup s_memrealtime phase stamps
 };
 
 }  // namespace lsd

@@ -5,20 +5,26 @@
 // logits[0,-1] / 0.6 -> topk(40) -> softmax -> multinomial).  Here only the
 // sampled id (int32) leaves the last stage.
 //
-// Per row (one 1024-thread block):
+// Per row, one 1024-thread block; every pass re-reads the row with 16-byte
+// loads (the row -- 200 KB for GPT-2, 500 KB for Llama-3 -- stays L2-resident
+// across passes).
 //   greedy: block argmax (lowest index on ties).
-//   top-k : 4-pass 8-bit radix select over order-preserving uint32 keys finds
-//           the k-th largest logit; the k winners are collected, sorted by
-//           (value desc, index asc) with a bitonic sort in LDS (deterministic
-//           order regardless of atomic arrival), softmax over value/T, and an
-//           inverse-CDF draw with u = splitmix64(seed * FNV + step) -- the same
-//           counter-based generator as runtime/batch.py:counter_uniform, so a
-//           seeded request reproduces across batch layouts and stage counts.
+//   top-k : radix select of the k-th largest order-preserving key in three
+//           passes over bits [31:20], [19:8], [7:0] (4096/4096/256 bins; the
+//           exponent-heavy top bits are spread over 4096 bins so LDS atomics
+//           do not pile onto a few hot bins), each bin search a block-parallel
+//           suffix scan.  The k winners are sorted by (value desc, index asc)
+//           with a bitonic network in LDS (deterministic regardless of atomic
+//           arrival order), softmax over value/T, inverse-CDF draw with
+//           u = splitmix64(seed * FNV + step) -- the same counter-based
+//           generator as runtime/batch.py:counter_uniform, so a seeded
+//           request reproduces across batch layouts and stage counts.
 #include "common.h"
 
 namespace lsd {
 
-constexpr int SMAX = 1024;  // max top_k supported on device (host validates)
+constexpr int SMAX = 1024;   // max top_k on device (host validates)
+constexpr int NT = 1024;     // threads per row
 
 __device__ __forceinline__ unsigned fkey(float x) {
   unsigned u = __float_as_uint(x);
@@ -38,29 +44,59 @@ __device__ __forceinline__ float counter_uniform(long long seed, long long step)
   return (float)((double)(z >> 40) / 16777216.0);
 }
 
-__global__ __launch_bounds__(1024) void sample_kernel(const float* __restrict__ logits, long ld,
-                                                      int V, const float* __restrict__ temp,
-                                                      const int* __restrict__ topk,
-                                                      const int* __restrict__ greedy,
-                                                      const long long* __restrict__ seeds,
-                                                      const long long* __restrict__ step,
-                                                      int* __restrict__ out) {
-  __shared__ unsigned hist[256];
-  __shared__ float cval[2 * SMAX];
-  __shared__ int cidx[2 * SMAX];
+// Block-wide inclusive suffix scan of one value per thread (thread t holds
+// the total of its bins; suffix = sum over threads >= t).  `tmp` >= 16 words.
+__device__ __forceinline__ unsigned block_suffix(unsigned v, unsigned* tmp) {
+  const int lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned s = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned o = __shfl_down(s, d, 64);
+    if (lane + d < 64) s += o;
+  }
+  __syncthreads();
+  if (lane == 0) tmp[w] = s;  // wave total
+  __syncthreads();
+  unsigned later = 0;
+  for (int j = w + 1; j < nw; ++j) later += tmp[j];
+  return s + later;
+}
+
+// Visit every (value, index) of the row: 4 consecutive values per thread per
+// step (row stride is a multiple of 64 floats, so the float4 never leaves it).
+template <typename F>
+__device__ __forceinline__ void for_row(const float* x, int V, F&& f) {
+  for (int b = threadIdx.x * 4; b < V; b += NT * 4) {
+    const f32x4 q = *reinterpret_cast<const f32x4*>(x + b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (b + j < V) f(q[j], b + j);
+  }
+}
+
+__global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ logits, long ld,
+                                                    int V, const float* __restrict__ temp,
+                                                    const int* __restrict__ topk,
+                                                    const int* __restrict__ greedy,
+                                                    const long long* __restrict__ seeds,
+                                                    const long long* __restrict__ step,
+                                                    int* __restrict__ out) {
+  __shared__ unsigned hist[4096];
+  __shared__ float cval[SMAX];
+  __shared__ int cidx[SMAX];
+  __shared__ unsigned tmp[32];
   __shared__ float redv[16];
   __shared__ int redi[16];
-  __shared__ unsigned s_prefix, s_need, s_ngt, s_neq;
+  __shared__ unsigned s_digit, s_need, s_cnt;
   const int row = blockIdx.x, tid = threadIdx.x;
   const float* x = logits + (long)row * ld;
 
   if (greedy[row]) {
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = tid; i < V; i += blockDim.x) {
-      const float v = x[i];
-      if (v > best || (v == best && i < bi)) { best = v; bi = i; }
-    }
+    for_row(x, V, [&](float val, int idx) {
+      if (val > best || (val == best && idx < bi)) { best = val; bi = idx; }
+    });
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
       const float ov = shfl_xor(best, m);
@@ -70,7 +106,7 @@ __global__ __launch_bounds__(1024) void sample_kernel(const float* __restrict__ 
     if (lane_id() == 0) { redv[tid >> 6] = best; redi[tid >> 6] = bi; }
     __syncthreads();
     if (tid == 0) {
-      for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+      for (int w = 1; w < NT / 64; ++w)
         if (redv[w] > best || (redv[w] == best && redi[w] < bi)) { best = redv[w]; bi = redi[w]; }
       out[row] = bi;
     }
@@ -78,98 +114,130 @@ __global__ __launch_bounds__(1024) void sample_kernel(const float* __restrict__ 
   }
 
   const int k = min(max(topk[row], 1), min(SMAX, V));
-  // ---- radix select: the k-th largest key
+  // ---- radix select over 12 + 12 + 8 bits
   unsigned prefix = 0, mask = 0, need = k;
-  for (int pass = 0; pass < 4; ++pass) {
-    const int shift = 24 - 8 * pass;
-    for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+  const int shifts[3] = {20, 8, 0};
+  const int widths[3] = {12, 12, 8};
+#pragma unroll
+  for (int pass = 0; pass < 3; ++pass) {
+    const int sh = shifts[pass], nb = 1 << widths[pass];
+    for (int i = tid; i < nb; i += NT) hist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < V; i += blockDim.x) {
-      const unsigned kk = fkey(x[i]);
-      if ((kk & mask) == prefix) atomicAdd(&hist[(kk >> shift) & 255u], 1u);
+    for_row(x, V, [&](float val, int) {
+      const unsigned kk = fkey(val);
+      if ((kk & mask) == prefix) atomicAdd(&hist[(kk >> sh) & (nb - 1)], 1u);
+    });
+    __syncthreads();
+    // thread t owns bins [t*bpt, (t+1)*bpt); find the bin where the count of
+    // keys in strictly higher bins is < need <= that plus the bin itself
+    const int bpt = (nb + NT - 1) / NT;
+    unsigned mine = 0;
+    for (int j = 0; j < bpt; ++j) {
+      const int b = tid * bpt + j;
+      if (b < nb) mine += hist[b];
     }
-    __syncthreads();
-    if (tid == 0) {
-      unsigned cum = 0;
-      int d = 255;
-      for (; d >= 0; --d) {
-        if (cum + hist[d] >= need) break;
-        cum += hist[d];
+    const unsigned suf = block_suffix(mine, tmp);  // keys in bins >= tid*bpt
+    const unsigned above = suf - mine;              // keys in bins > my range
+    if (above < need && suf >= need) {
+      unsigned cum = above;
+      for (int j = bpt - 1; j >= 0; --j) {
+        const int b = tid * bpt + j;
+        if (b >= nb) continue;
+        if (cum + hist[b] >= need) { s_digit = b; s_need = need - cum; break; }
+        cum += hist[b];
       }
-      s_prefix = prefix | ((unsigned)d << shift);
-      s_need = need - cum;
     }
     __syncthreads();
-    prefix = s_prefix;
+    prefix |= s_digit << sh;
     need = s_need;
-    mask |= 255u << shift;
+    mask |= (unsigned)(nb - 1) << sh;
     __syncthreads();
   }
-  // keys > prefix: k - need of them; keys == prefix: take the `need` lowest indices
-  if (tid == 0) { s_ngt = 0; s_neq = 0; }
+  // ---- collect: keys > prefix (k - need of them) and the `need` lowest-index
+  // keys == prefix.  Equal keys are rare; take them in index order.
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  for_row(x, V, [&](float val, int idx) {
+    if (fkey(val) > prefix) {
+      const unsigned slot = atomicAdd(&s_cnt, 1u);
+      cval[slot] = val;
+      cidx[slot] = idx;
+    }
+  });
   __syncthreads();
   const unsigned n_gt = k - need;
-  for (int i = tid; i < V; i += blockDim.x) {
-    const unsigned kk = fkey(x[i]);
-    if (kk > prefix) {
-      const unsigned slot = atomicAdd(&s_ngt, 1u);
-      cval[slot] = x[i];
-      cidx[slot] = i;
-    } else if (kk == prefix) {
-      const unsigned slot = atomicAdd(&s_neq, 1u);
-      if (slot < (unsigned)SMAX) { cval[SMAX + slot] = x[i]; cidx[SMAX + slot] = i; }
-    }
-  }
-  __syncthreads();
-  // equal keys: keep the `need` smallest indices (selection by thread 0; ties are rare)
-  if (tid == 0) {
-    const unsigned neq = min(s_neq, (unsigned)SMAX);
+  if (need > 0) {
+    // index-ordered scan of equal keys: each pass takes the smallest index left
     for (unsigned a = 0; a < need; ++a) {
-      unsigned best = a;
-      for (unsigned b2 = a + 1; b2 < neq; ++b2)
-        if (cidx[SMAX + b2] < cidx[SMAX + best]) best = b2;
-      const int ti = cidx[SMAX + a]; cidx[SMAX + a] = cidx[SMAX + best]; cidx[SMAX + best] = ti;
-      const float tv = cval[SMAX + a]; cval[SMAX + a] = cval[SMAX + best]; cval[SMAX + best] = tv;
-      cval[n_gt + a] = cval[SMAX + a];
-      cidx[n_gt + a] = cidx[SMAX + a];
+      int my_best = 0x7fffffff;
+      const int prev = a == 0 ? -1 : cidx[n_gt + a - 1];
+      for_row(x, V, [&](float val, int idx) {
+        if (idx > prev && fkey(val) == prefix) my_best = min(my_best, idx);
+      });
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) my_best = min(my_best, shfl_xor(my_best, m));
+      if (lane_id() == 0) redi[tid >> 6] = my_best;
+      __syncthreads();
+      if (tid == 0) {
+        int b = redi[0];
+        for (int w = 1; w < NT / 64; ++w) b = min(b, redi[w]);
+        cidx[n_gt + a] = b;
+        cval[n_gt + a] = x[b];
+      }
+      __syncthreads();
     }
   }
-  __syncthreads();
   // ---- bitonic sort of the k winners: (value desc, index asc); pad to pow2
   int n2 = 1;
   while (n2 < k) n2 <<= 1;
-  for (int i = k + tid; i < n2; i += blockDim.x) { cval[i] = -INFINITY; cidx[i] = 0x7fffffff; }
+  for (int i = k + tid; i < n2; i += NT) { cval[i] = -INFINITY; cidx[i] = 0x7fffffff; }
   __syncthreads();
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < n2; i += blockDim.x) {
+      for (int i = tid; i < n2; i += NT) {
         const int j = i ^ stride;
         if (j > i) {
-          const bool up = (i & size) == 0;  // "up" = descending by our order
+          const bool up = (i & size) == 0;
           const float vi = cval[i], vj = cval[j];
           const int ii = cidx[i], ij = cidx[j];
           const bool i_first = (vi > vj) || (vi == vj && ii < ij);
-          if (up != i_first) {
-            cval[i] = vj; cval[j] = vi; cidx[i] = ij; cidx[j] = ii;
-          }
+          if (up != i_first) { cval[i] = vj; cval[j] = vi; cidx[i] = ij; cidx[j] = ii; }
         }
       }
       __syncthreads();
     }
   }
-  // ---- softmax over value/T and inverse-CDF draw
-  if (tid == 0) {
+  // ---- softmax over value/T and inverse-CDF draw (one wave, k <= 1024)
+  if (tid < 64) {
     const float T = temp[row];
     const float x0 = cval[0] / T;
+    // running CDF in chunks of 64: lane l owns element base + l
+    const float u = counter_uniform(seeds[row], step[row]);
     float tot = 0.f;
-    for (int i = 0; i < k; ++i) {
-      tot += __expf(cval[i] / T - x0);
-      cval[SMAX + i] = tot;  // running (unnormalised) CDF
+    for (int base = 0; base < k; base += 64) {
+      const int i = base + tid;
+      const float e = i < k ? __expf(cval[i] / T - x0) : 0.f;
+      tot += wave_sum(e);
     }
-    const float u = counter_uniform(seeds[row], step[row]) * tot;
-    int j = 0;
-    while (j < k - 1 && cval[SMAX + j] < u) ++j;
-    out[row] = cidx[j];
+    const float target = u * tot;
+    float run = 0.f;
+    int pick = k - 1;
+    for (int base = 0; base < k; base += 64) {
+      const int i = base + tid;
+      float e = i < k ? __expf(cval[i] / T - x0) : 0.f;
+      // inclusive prefix within the wave
+      float pre = e;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const float o = __shfl_up(pre, d, 64);
+        if (tid >= d) pre += o;
+      }
+      const float c = run + pre;
+      const unsigned long long hit = __ballot(i < k && c >= target);
+      if (hit) { pick = base + __builtin_ctzll(hit); break; }
+      run += __shfl(pre, 63, 64);
+    }
+    if (tid == 0) out[row] = cidx[pick];
   }
 }
 
@@ -181,7 +249,8 @@ extern "C" hipError_t lsd_sample(const float* logits, long ld, int B, int V, con
                                  const int* topk, const int* greedy, const long long* seeds,
                                  const long long* step, int* out, hipStream_t st) {
   if (B == 0) return hipSuccess;
-  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(1024), 0, st, logits, ld, V, temp, topk, greedy,
+  if (ld % 4 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(NT), 0, st, logits, ld, V, temp, topk, greedy,
                      seeds, step, out);
   return hipGetLastError();
 }

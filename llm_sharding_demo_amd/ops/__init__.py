@@ -113,7 +113,6 @@ class ReferenceBackend(Backend):
 
 
 _REFERENCE = ReferenceBackend()
-_HIP = None
 
 
 def hip_available() -> bool:
@@ -125,11 +124,9 @@ def hip_available() -> bool:
 
 
 def get_backend(device) -> Backend:
-    global _HIP
     dev = torch.device(device)
     if dev.type == "cpu":
         return _REFERENCE
-    if _HIP is None:
-        from .hip import HipBackend  # raises loudly if the extension is missing
-        _HIP = HipBackend()
-    return _HIP
+    from .hip import HipBackend  # raises loudly if the extension is missing
+
+    return HipBackend()  # one per stage: owns that stage's split-K counters / tables

@@ -16,6 +16,7 @@ Device weight layout (set up once per stage by `prepare_stage`):
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -80,9 +81,14 @@ def prefill_tiles(meta) -> torch.Tensor:
 class HipBackend(Backend):
     name = "hip"
     TARGET_BLOCKS = 512  # >> 256 CUs so every CU streams
+    # decode GEMM: aim for this many workgroups (column tiles x k-splits)
+    SK_TARGET = int(os.environ.get("LSD_SK_TARGET", "384"))
+    SK_MIN_STEPS = int(os.environ.get("LSD_SK_MIN_STEPS", "2"))  # 32-k steps per split
 
     def __init__(self):
         self.C = _load()
+        self.counters = None
+        self._rope = None
 
     # ------------------------------------------------------------------
     def prepare_stage(self, stage) -> None:
@@ -105,6 +111,8 @@ class HipBackend(Backend):
         else:
             stage._rope = None
         self._rope = getattr(stage, "_rope", None)
+        # split-K ticket counters: zero at rest, re-armed by each tile's last arriver
+        self.counters = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
         stage._hip_prepared = True
 
     # ------------------------------------------------------------------
@@ -116,8 +124,16 @@ class HipBackend(Backend):
         if self._tiled(M):
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
             return max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
-        blocks = N // 16
-        return max(1, min(math.ceil(self.TARGET_BLOCKS / blocks), K // 32 // 8 or 1))
+        return self._sk_splits(N, K)
+
+    def _sk_splits(self, N: int, K: int, nw: int = 1) -> int:
+        tiles = N // (64 * nw)
+        return max(1, min(math.ceil(self.SK_TARGET / tiles), K // 32 // self.SK_MIN_STEPS or 1))
+
+    def _gemm_kw(self, M: int, N: int, K: int, nw: int = 1):
+        if self._tiled(M):
+            return True, 1
+        return False, self._sk_splits(N, K, nw)
 
     # ------------------------------------------------------------------
     def embed(self, ids, pos, wte, wpe):
@@ -151,9 +167,10 @@ class HipBackend(Backend):
         return self.C.norm(x, None, None, w, b, eps, rms, rows, True)
 
     def qkv_kv_append(self, xn, w, b, cache_k, cache_v, meta, mcfg):
+        tiled, splits = self._gemm_kw(xn.shape[0], w.shape[0], w.shape[1])
         return self.C.linear_qkv(xn, w, b, cache_k, cache_v, meta.token_slots, meta.token_pos,
                                  mcfg.q_size, mcfg.kv_size, mcfg.head_dim, self._rope,
-                                 self._tiled(xn.shape[0]))
+                                 tiled, splits, self.counters)
 
     def attention(self, q, cache_k, cache_v, meta):
         n_kv, hd = cache_k.shape[1], cache_k.shape[3]
@@ -173,18 +190,20 @@ class HipBackend(Backend):
 
     def linear(self, a, w, b=None, act: str = "none"):
         code = {"none": 0, "gelu": 1, "silu_mul": 2}[act]
-        return self.C.linear(a, w, b, code, self._tiled(a.shape[0]))
+        tiled, splits = self._gemm_kw(a.shape[0], w.shape[0], w.shape[1], 2 if code == 2 else 1)
+        return self.C.linear(a, w, b, code, tiled, splits, self.counters)
 
     def linear_residual(self, a, w, b, r: Residual) -> None:
         M, K = a.shape
         N = w.shape[0]
         splits = self._resid_splits(M, N, K)
-        slab = self.C.linear_residual(a, w, b, r.x, splits, self._tiled(M))
+        slab = self.C.linear_residual(a, w, b, r.x, splits, self._tiled(M), self.counters)
         if slab is not None:
             r.pending.append((slab, b))
 
     def logits(self, xn, w):
-        return self.C.linear_f32(xn, w, self._tiled(xn.shape[0]))
+        tiled, splits = self._gemm_kw(xn.shape[0], w.shape[0], w.shape[1])
+        return self.C.linear_f32(xn, w, tiled, splits, self.counters)
 
     def sample(self, logits, samp, vocab: int):
         return self.C.sample(logits, vocab, samp.temperature, samp.top_k, samp.greedy,

@@ -26,6 +26,7 @@ all positions / sampler counters advance on the device inside the graph.
 """
 from __future__ import annotations
 
+import threading
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -35,6 +36,9 @@ import torch
 from ..models.stage import StageModel
 from ..runtime.batch import BatchMeta, SamplingState
 from .comm import Handle, SendHandle, Transport
+
+
+_CAPTURE_LOCK = threading.Lock()
 
 
 @dataclass
@@ -77,14 +81,25 @@ class StageWorker:
         self.first = stage_idx == 0
         self.last = stage_idx == num_stages - 1
         self.H = stage.cfg.hidden
-        self.stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        # Each stage worker owns a non-blocking stream: no device-wide syncs, so
+        # one stage may capture a hipGraph while another (same GPU) keeps running.
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------
     def _sync(self) -> None:
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+        if self.stream is not None:
+            self.stream.synchronize()
 
     def run_round(self, spec: RoundSpec) -> Optional[RoundResult]:
+        if self.stream is None:
+            return self._run_round(spec)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            res = self._run_round(spec)
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        return res
+
+    def _run_round(self, spec: RoundSpec) -> Optional[RoundResult]:
         st, dev, P, r = self.stage, self.device, self.P, self.r
         mbs = spec.microbatches
         M, G = len(mbs), spec.steps
@@ -223,11 +238,18 @@ class StageWorker:
     def _capture(self, fn):
         """Capture one decode step (this stage's forward for one microbatch,
         plus sampling on the last stage) into a hipGraph."""
+        # capture_begin/end directly: torch.cuda.graph() does a device-wide
+        # synchronize on entry, which is illegal while a sibling stage thread on
+        # the same GPU is capturing.  One capture at a time per process.
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                out = fn()
+        with _CAPTURE_LOCK:
+            with torch.cuda.stream(s):
+                g.capture_begin(capture_error_mode="thread_local")
+                try:
+                    out = fn()
+                finally:
+                    g.capture_end()
         torch.cuda.current_stream(self.device).wait_stream(s)
         return g, out

@@ -56,43 +56,60 @@ def test_norm_with_slab_combine(C, H, rms):
     close(y2, y_ref[rows.long()], 2e-2)
 
 
+@pytest.fixture(scope="module")
+def CNT():
+    return torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+
+
 @pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 65, 200])
 @pytest.mark.parametrize("act", ["none", "gelu", "silu_mul"])
-def test_linear(C, M, act):
+@pytest.mark.parametrize("splits", [1, 3, 7])
+def test_linear(C, CNT, M, act, splits):
     from llm_sharding_demo_amd.ops.hip import interleave_gate_up
 
     N, K = 384, 640
     a, w, bias = bf(M, K, seed=5), bf(N, K, scale=0.05, seed=6), bf(N, scale=0.1, seed=7)
     tiled = M > 64
+    sp = 1 if tiled else splits
     if act == "silu_mul":
-        y = C.linear(a, interleave_gate_up(w, N // 2).contiguous(), None, 2, tiled)
+        N = 256
+        w = w[:N].contiguous()
+        y = C.linear(a, interleave_gate_up(w, N // 2).contiguous(), None, 2, tiled, sp, CNT)
         y_ref = ref.silu_mul(*ref.linear(a, w).split(N // 2, 1))
     else:
-        y = C.linear(a, w, bias, 1 if act == "gelu" else 0, tiled)
+        y = C.linear(a, w, bias, 1 if act == "gelu" else 0, tiled, sp, CNT)
         y_ref = ref.linear(a, w, bias)
         if act == "gelu":
             y_ref = ref.gelu_new(y_ref)
     close(y, y_ref, 3e-2)
+    assert int(CNT.abs().sum()) == 0  # every ticket counter re-armed
 
 
-@pytest.mark.parametrize("M,splits", [(3, 1), (16, 4), (64, 5), (100, 1), (130, 3)])
-def test_linear_residual_and_f32(C, M, splits):
+@pytest.mark.parametrize("M,splits", [(3, 1), (16, 4), (64, 5), (64, 16), (100, 1), (130, 3)])
+def test_linear_residual_and_f32(C, CNT, M, splits):
     N, K = 256, 1024
     a, w, bias = bf(M, K, seed=8), bf(N, K, scale=0.05, seed=9), bf(N, scale=0.1, seed=10)
     tiled = M > 64
     x = torch.randn(M, N, device=DEV)
     x_ref = x + ref.linear(a, w, bias)
-    slab = C.linear_residual(a, w, bias, x, splits, tiled)
+    slab = C.linear_residual(a, w, bias, x, splits, tiled, CNT)
     if slab is not None:
         C.norm(x, slab, bias, None, None, 0.0, True, None, False)
     close(x, x_ref, 2e-3, 1e-3)
-    close(C.linear_f32(a, w, tiled), ref.linear(a, w), 2e-3, 1e-3)
+    close(C.linear_f32(a, w, tiled, 1 if tiled else splits, CNT), ref.linear(a, w), 2e-3, 1e-3)
 
 
-def test_gemm_large_prefill_shape(C):
+def test_split_k_deterministic(C, CNT):
+    a, w = bf(64, 1600, seed=30), bf(4800, 1600, scale=0.03, seed=31)
+    y1 = C.linear(a, w, None, 0, False, 7, CNT)
+    for _ in range(5):
+        assert torch.equal(C.linear(a, w, None, 0, False, 7, CNT), y1)
+
+
+def test_gemm_large_prefill_shape(C, CNT):
     M, N, K = 1000, 4800, 1600
     a, w = bf(M, K, seed=11), bf(N, K, scale=0.03, seed=12)
-    close(C.linear(a, w, None, 0, True), ref.linear(a, w), 3e-2)
+    close(C.linear(a, w, None, 0, True, 1, CNT), ref.linear(a, w), 3e-2)
 
 
 def _cache(slots, n_kv, S, hd):
@@ -101,7 +118,8 @@ def _cache(slots, n_kv, S, hd):
 
 
 @pytest.mark.parametrize("rope", [False, True])
-def test_qkv_kv_append(C, rope):
+@pytest.mark.parametrize("splits", [1, 4])
+def test_qkv_kv_append(C, CNT, rope, splits):
     from llm_sharding_demo_amd.ops.hip import rope_pair_permutation, rope_table
 
     nh, n_kv, hd, H = 4, 2, 64, 256
@@ -123,14 +141,14 @@ def test_qkv_kv_append(C, rope):
                           torch.arange(qs + kvs, qs + 2 * kvs)]).to(DEV)
         w, bias = w[perm].contiguous(), bias[perm].contiguous()
         table = rope_table(S, hd, 10000.0, DEV)
-        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, table, False)
+        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, table, False, splits, CNT)
         # un-permute the pair-interleaved head dims for comparison
         p1 = rope_pair_permutation(1, hd)
         inv = torch.argsort(p1).to(DEV)
         q = q.reshape(T, nh, hd)[:, :, inv]
         kc = kc[..., inv]
     else:
-        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, None, False).reshape(T, nh, hd)
+        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, None, False, splits, CNT).reshape(T, nh, hd)
     ref.kv_append(kr, vr, k_ref, v_ref, tslot, tpos)
     close(q, q_ref, 3e-2)
     close(kc, kr, 3e-2)

@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Per-kernel microbenchmarks on one MI355X (events, warm L2 excluded where it
+matters by rotating through several weight copies > 256 MiB Infinity Cache).
+
+Prints one line per case: time (us), achieved bandwidth (TB/s, weight+KV bytes
+streamed), and for GEMMs the torch.matmul (hipBLASLt) time on the same data as
+a yardstick.  Output also written as JSON to gpurun_out/microbench.json.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llm_sharding_demo_amd.ops.hip import _load, prefill_tiles  # noqa: E402
+from llm_sharding_demo_amd.runtime.batch import BatchMeta  # noqa: E402
+
+C = _load()
+DEV = "cuda"
+RESULTS = []
+
+
+def timeit(fn, iters=50, warm=3, graph=True):
+    """Device time per call.  graph=True captures `iters` calls into one
+    hipGraph and replays it, so host launch overhead does not bound the
+    number (matches how the engine runs decode)."""
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        for _ in range(warm):
+            fn()
+    torch.cuda.current_stream().wait_stream(st)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        s.record()
+        g.replay()
+        e.record()
+    else:
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1e3 / iters  # us
+
+
+def rotating(make, nbytes_each, total=640 << 20):
+    n = max(2, math.ceil(total / max(nbytes_each, 1)))
+    return [make() for _ in range(n)]
+
+
+def report(name, us, nbytes, extra=None):
+    tbs = nbytes / (us * 1e-6) / 1e12
+    row = {"case": name, "us": round(us, 2), "TB/s": round(tbs, 3)}
+    if extra:
+        row.update(extra)
+    RESULTS.append(row)
+    print(json.dumps(row), flush=True)
+
+
+def bench_gemm(M, N, K, act=0, resid=False, label=""):
+    ws = rotating(lambda: torch.randn(N, K, device=DEV).bfloat16(), N * K * 2)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    x = torch.randn(M, N, device=DEV)
+    it = [0]
+    tiled = M > 64
+    be = __import__("llm_sharding_demo_amd.ops.hip", fromlist=["HipBackend"]).HipBackend()
+
+    be.counters = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    nw = 2 if act == 2 else 1
+    tiled_, splits = be._gemm_kw(M, N, K, nw)
+
+    def run():
+        w = ws[it[0] % len(ws)]
+        it[0] += 1
+        if resid:
+            C.linear_residual(a, w, None, x, be._resid_splits(M, N, K), tiled, be.counters)
+        else:
+            C.linear(a, w, None, act, tiled, splits, be.counters)
+
+    us = timeit(run)
+    it[0] = 0
+
+    def tm():
+        w = ws[it[0] % len(ws)]
+        it[0] += 1
+        torch.matmul(a, w.t())
+
+    ut = timeit(tm)
+    report(f"gemm{label} M={M} N={N} K={K} S={splits}", us, N * K * 2, {"hipblaslt_us": round(ut, 2)})
+
+
+def bench_attn_decode(B, nh, n_kv, hd, ctx, slots=None):
+    slots = slots or B
+    S = ctx + 1
+    kc = torch.randn(slots, n_kv, S, hd, device=DEV).bfloat16()
+    vc = torch.randn(slots, n_kv, S, hd, device=DEV).bfloat16()
+    q = torch.randn(B, nh * hd, device=DEV).bfloat16()
+    ss = torch.arange(B, dtype=torch.int32, device=DEV)
+    pos = torch.full((B,), ctx - 1, dtype=torch.int32, device=DEV)
+    splits = 1 if B * n_kv >= 512 else min(math.ceil(512 / (B * n_kv)), max(1, math.ceil(ctx / 256)))
+    us = timeit(lambda: C.attn_decode(q, kc, vc, ss, pos, nh, splits))
+    report(f"attn_decode B={B} nh={nh} kv={n_kv} hd={hd} ctx={ctx} splits={splits}", us,
+           B * n_kv * ctx * hd * 2 * 2)
+
+
+def bench_attn_prefill(nseq, L, nh, n_kv, hd):
+    kc = torch.randn(nseq, n_kv, L, hd, device=DEV).bfloat16()
+    vc = torch.randn(nseq, n_kv, L, hd, device=DEV).bfloat16()
+    meta = BatchMeta.build(list(range(nseq)), [0] * nseq, [L] * nseq, DEV)
+    q = torch.randn(meta.num_tokens, nh * hd, device=DEV).bfloat16()
+    tiles = prefill_tiles(meta).to(DEV)
+    us = timeit(lambda: C.attn_prefill(q, kc, vc, tiles, meta.seq_slots, meta.q_start, meta.cu_q, nh))
+    flops = nseq * nh * 2 * 2 * hd * L * L / 2
+    report(f"attn_prefill seqs={nseq} L={L} nh={nh} hd={hd}", us, 0, {"TFLOP/s": round(flops / us / 1e6, 1)})
+
+
+def bench_norm(T, H, splits):
+    x = torch.randn(T, H, device=DEV)
+    slab = torch.randn(splits, T, H, device=DEV) if splits else None
+    w = torch.ones(H, device=DEV).bfloat16()
+    b = torch.zeros(H, device=DEV).bfloat16()
+    us = timeit(lambda: C.norm(x, slab, None, w, b, 1e-5, False, None, True))
+    report(f"norm T={T} H={H} slabs={splits}", us, T * H * 4 * (2 + splits))
+
+
+def bench_sample(B, V, greedy):
+    Vp = (V + 63) // 64 * 64
+    lg = torch.randn(B, Vp, device=DEV) * 3
+    t = torch.full((B,), 0.6, device=DEV)
+    k = torch.full((B,), 40, dtype=torch.int32, device=DEV)
+    g = torch.full((B,), int(greedy), dtype=torch.int32, device=DEV)
+    sd = torch.arange(B, dtype=torch.int64, device=DEV)
+    st = torch.zeros(B, dtype=torch.int64, device=DEV)
+    us = timeit(lambda: C.sample(lg, V, t, k, g, sd, st))
+    report(f"sample B={B} V={V} greedy={greedy}", us, B * V * 4)
+
+
+def stamps_gemm(M, N, K, splits, act=0, label=""):
+    """Per-workgroup phase timeline of one decode-GEMM launch (diagnostic)."""
+    w = torch.randn(N, K, device=DEV).bfloat16()
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    nb = (N // 64) * splits
+    st = torch.zeros(nb * 8, dtype=torch.int64, device=DEV)
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=DEV)
+    for rep in range(3):
+        flush.zero_()  # evict W from the Infinity Cache
+        torch.cuda.synchronize()
+        st.zero_()
+        C.set_stamps(st)
+        C.linear(a, w, None, act, False, splits, cnt)
+        torch.cuda.synchronize()
+        C.set_stamps(None)
+    t = st.view(nb, 8).cpu().double()
+    t0 = t[:, 0].min()
+    ph = {}
+    ent = (t[:, 0] - t0) * 10 / 1000  # us (100 MHz)
+    lat = (t[:, 1] - t[:, 0]) * 10 / 1000
+    comp = (t[:, 2] - t[:, 1]) * 10 / 1000
+    pub = (t[:, 3] - t[:, 2]) * 10 / 1000
+    last = t[:, 5] > 0
+    red = (t[last, 4] - t[last, 3]) * 10 / 1000
+    epi = (t[last, 5] - t[last, 4]) * 10 / 1000
+    end = (t[last, 5] - t0) * 10 / 1000
+    q = lambda x: [round(float(x.quantile(v)), 2) for v in (0.0, 0.5, 0.9, 1.0)] if x.numel() else []
+    row = {"case": f"stamps{label} M={M} N={N} K={K} S={splits} blocks={nb}",
+           "entry_us": q(ent), "load_us": q(lat), "compute_us": q(comp), "publish_us": q(pub),
+           "reduce_us": q(red), "epilogue_us": q(epi), "span_us": round(float(end.max()), 2),
+           "xcc_hist": torch.bincount(t[:, 7].long(), minlength=8).tolist()}
+    RESULTS.append(row)
+    print(json.dumps(row), flush=True)
+
+
+def main():
+    which = sys.argv[1:] or ["gemm", "attn", "norm", "sample"]
+    if "stamps" in which:
+        for M, S in ((16, 1), (16, 4), (64, 1), (64, 4), (64, 8)):
+            stamps_gemm(M, 4800, 1600, S, label="_qkv")
+        for M, S in ((64, 1), (64, 6), (64, 16)):
+            stamps_gemm(M, 1600, 1600, S, label="_proj")
+        stamps_gemm(64, 50304, 1600, 1, label="_lmhead")
+    H, F, V = 1600, 6400, 50304
+    if "sweep" in which:
+        from llm_sharding_demo_amd.ops.hip import HipBackend
+        for tgt in (128, 256, 384, 512, 768, 1024):
+            HipBackend.SK_TARGET = tgt
+            print("SK_TARGET", tgt, flush=True)
+            for M in (16, 64):
+                bench_gemm(M, 3 * H, H, label="_qkv")
+                bench_gemm(M, F, H, act=1, label="_fc")
+                bench_gemm(M, H, H, resid=True, label="_proj")
+                bench_gemm(M, H, F, resid=True, label="_proj2")
+                bench_gemm(M, V, H, label="_lmhead")
+        HipBackend.SK_TARGET = 384
+    if "gemm" in which:
+        for M in (1, 16, 32, 64, 128, 256):
+            bench_gemm(M, 3 * H, H, label="_qkv")
+            bench_gemm(M, F, H, act=1, label="_fc")
+            bench_gemm(M, H, H, resid=True, label="_proj")
+            bench_gemm(M, H, F, resid=True, label="_proj2")
+        for M in (1, 64):
+            bench_gemm(M, V, H, act=0, label="_lmhead")
+        bench_gemm(8192, 3 * H, H, label="_prefill_qkv")
+    if "attn" in which:
+        for B in (1, 16, 64):
+            bench_attn_decode(B, 25, 25, 64, 192)
+        bench_attn_decode(64, 25, 25, 64, 1024)
+        bench_attn_decode(64, 32, 8, 128, 512)
+        bench_attn_prefill(64, 128, 25, 25, 64)
+        bench_attn_prefill(4, 1024, 25, 25, 64)
+        bench_attn_prefill(4, 1024, 32, 8, 128)
+    if "norm" in which:
+        for s in (0, 4, 6):
+            bench_norm(64, H, s)
+    if "sample" in which:
+        for g in (True, False):
+            bench_sample(64, 50257, g)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/microbench.json", "w") as f:
+        json.dump(RESULTS, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
