@@ -4,8 +4,9 @@ pipeline at N stages = N MI355X (BASELINE.json "metric").
 
 One step = one complete generation round, end to end: prefill of every
 prompt, then `--gen` decode steps, for a global batch of N x --batch
-sequences split into microbatches that flow through the N-stage pipeline
-(one stage per GPU, RCCL p2p between stages).  Weak scaling: each GPU holds
+sequences split into 2N microbatches that flow through the N-stage pipeline
+(one stage per GPU, RCCL p2p between stages; each stage keeps two
+microbatches in flight on two HIP streams).  Weak scaling: each GPU holds
 1/N of the layers and the global batch grows with N.  Nothing is skipped in
 the timed region: prefill, every layer, lm_head and the sampler (reference
 sampler: T=0.6, top-k=40; --greedy for argmax) run for every token.
@@ -36,10 +37,14 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--model", default="gpt2-xl")
-    p.add_argument("--batch", type=int, default=64, help="sequences per GPU (per microbatch)")
+    p.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "128")),
+                   help="sequences per GPU")
     p.add_argument("--prompt", type=int, default=128)
     p.add_argument("--gen", type=int, default=128)
-    p.add_argument("--microbatches", type=int, default=0, help="0 -> N (one per stage)")
+    p.add_argument("--microbatches", type=int, default=int(os.environ.get("BENCH_MB", "0")),
+                   help="0 -> 2N: two 64-sequence microbatches in flight per stage")
+    p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),
+                   help="nccl (RCCL over xGMI) | gloo (host-staged, for rehearsals)")
     p.add_argument("--greedy", action="store_true")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--seed", type=int, default=0)
@@ -57,12 +62,12 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != N:
         raise SystemExit(f"--gpus {N} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    M = args.microbatches or N
+    M = args.microbatches or 2 * N
     B = N * args.batch
     cfg = EngineConfig(model_id=args.model, num_stages=N, max_batch=B,
                        max_seq_len=args.prompt + args.gen, device="cuda",
                        use_graphs=not args.no_graphs, num_microbatches=M, seed=args.seed,
-                       transport="nccl")
+                       transport=args.transport)
     eng = Engine(cfg, mode="dist" if N > 1 else "local")
     rank = eng.rank
     worker = eng.workers[0]

@@ -191,35 +191,51 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
       const int kk = min((k0 + c * 4) * 32 + lch * 8, p.K - 8);
       glds16(p.A + (long)min(row, p.M - 1) * p.lda + kk, smem + c * CHUNK_BYTES + q * 1024);
     }
+    // All W fragments of the round are issued back to back.  No per-load guard:
+    // a runtime "if (j < nst) load" makes hipcc branch around each load and
+    // wait vmcnt(0) per element (guide §5 trap (c)); steps past the round end
+    // re-load the last valid step and are never consumed.
     bf16x8 wv[SK_ROUND_STEPS][NW];
 #pragma unroll
     for (int j = 0; j < SK_ROUND_STEPS; ++j)
-      if (j < nst)
 #pragma unroll
-        for (int ns = 0; ns < NW; ++ns) wv[j][ns] = ld8(wrow[ns] + (long)(k0 + j) * 32);
+      for (int ns = 0; ns < NW; ++ns) wv[j][ns] = ld8(wrow[ns] + (long)(k0 + min(j, nst - 1)) * 32);
     __syncthreads();  // vmcnt(0): the A image and this wave's W fragments have landed
     if (k0 == kb) { LSD_STAMP(1) }
-    auto step = [&](int j) {
+    // A fragments come from LDS one step ahead of the MFMAs that use them, so
+    // the ds_read latency of step j+1 hides under step j's MFMAs for any round
+    // length (the round count nst is wave-uniform).
+    auto read_a = [&](int j, bf16x8 (&a)[MT]) {
       const char* img = smem + (j >> 2) * CHUNK_BYTES;
       const int lch = (j & 3) * 4 + g;
-      bf16x8 a[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int row = mt * 16 + r;
         a[mt] = *reinterpret_cast<const bf16x8*>(img + row * 256 + ((lch ^ (row & 15)) << 4));
       }
+    };
+    // Fully unrolled (static indices keep wv[] in VGPRs -- a rolled loop sends
+    // it to scratch, guide rule 20) and branch-free.
+    bf16x8 a_cur[MT];
+    read_a(0, a_cur);
+#pragma unroll
+    for (int j = 0; j < SK_ROUND_STEPS; ++j) {
+      bf16x8 a_nxt[MT];
+      read_a(min(j + 1, nst - 1), a_nxt);
+      // Steps past the round end multiply a zeroed W fragment (A there is a
+      // valid, finite LDS row) -- no branch, so the accumulators stay in AGPRs.
+#pragma unroll
+      for (int ns = 0; ns < NW; ++ns) {
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        const u32x4 wb = __builtin_bit_cast(u32x4, wv[j][ns]);
+        wv[j][ns] = __builtin_bit_cast(bf16x8, j < nst ? wb : z);
+      }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int ns = 0; ns < NW; ++ns) acc[mt][ns] = mfma16(a[mt], wv[j][ns], acc[mt][ns]);
-    };
-    if (nst == SK_ROUND_STEPS) {  // common case: no guards, the scheduler can hoist ds_reads
+        for (int ns = 0; ns < NW; ++ns) acc[mt][ns] = mfma16(a_cur[mt], wv[j][ns], acc[mt][ns]);
 #pragma unroll
-      for (int j = 0; j < SK_ROUND_STEPS; ++j) step(j);
-    } else {
-#pragma unroll
-      for (int j = 0; j < SK_ROUND_STEPS; ++j)
-        if (j < nst) step(j);
+      for (int mt = 0; mt < MT; ++mt) a_cur[mt] = a_nxt[mt];
     }
     __syncthreads();  // the image is rewritten by the next round
   }

@@ -89,6 +89,7 @@ class HipBackend(Backend):
         self.C = _load()
         self.counters = None
         self._rope = None
+        self.lane = 0  # microbatch lane (stream) currently being issued; see pipeline.py
 
     # ------------------------------------------------------------------
     def prepare_stage(self, stage) -> None:
@@ -111,9 +112,18 @@ class HipBackend(Backend):
         else:
             stage._rope = None
         self._rope = getattr(stage, "_rope", None)
-        # split-K ticket counters: zero at rest, re-armed by each tile's last arriver
-        self.counters = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+        # split-K ticket counters: zero at rest, re-armed by each tile's last
+        # arriver; one row per microbatch lane so concurrent lanes never share one
+        self._counters = torch.zeros(8, 1 << 16, dtype=torch.int32, device=dev)
         stage._hip_prepared = True
+
+    @property
+    def counters(self):
+        return None if self._counters is None else self._counters[self.lane % 8]
+
+    @counters.setter
+    def counters(self, value):
+        self._counters = None if value is None else value.reshape(-1, 1 << 16)
 
     # ------------------------------------------------------------------
     @staticmethod

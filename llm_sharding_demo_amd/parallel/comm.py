@@ -272,9 +272,12 @@ def init_distributed(backend: str, device_type: str) -> None:
         return
     kw = {}
     if device_type == "cuda":
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # one rank per GPU; more ranks than GPUs (single-GPU rehearsal over
+        # gloo) wrap around.  device_count() does not initialise HIP.
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        kw["device_id"] = torch.device("cuda", local)
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
     dist.init_process_group(backend=backend, **kw)
 
 

@@ -26,6 +26,8 @@ all positions / sampler counters advance on the device inside the graph.
 """
 from __future__ import annotations
 
+import contextlib
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -84,6 +86,14 @@ class StageWorker:
         # Each stage worker owns a non-blocking stream: no device-wide syncs, so
         # one stage may capture a hipGraph while another (same GPU) keeps running.
         self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        # Microbatch "lanes": microbatch m of this stage runs on lanes[m % L], so
+        # independent microbatches overlap on the GPU -- one's latency-bound
+        # phases (small GEMMs, split-K tails) run beside another's bandwidth-
+        # bound ones (attention over the KV cache).  Each lane has its own
+        # split-K ticket counters in the backend.
+        n_lanes = int(os.environ.get("LSD_LANES", "2"))
+        self.lanes = ([torch.cuda.Stream(self.device) for _ in range(n_lanes)]
+                      if self.device.type == "cuda" else [])
 
     # ------------------------------------------------------------------
     def _sync(self) -> None:
@@ -129,6 +139,15 @@ class StageWorker:
                 in_pre.append(torch.empty(sum(lens), self.H, dtype=torch.float32, device=dev))
                 in_dec.append(torch.empty(mb.size, self.H, dtype=torch.float32, device=dev))
 
+        L = max(1, len(self.lanes))
+        for lane in self.lanes:
+            lane.wait_stream(torch.cuda.current_stream(dev))
+
+        def on_lane(m):
+            if not self.lanes:
+                return contextlib.nullcontext()
+            return torch.cuda.stream(self.lanes[m % L])
+
         items = [(s, m) for s in range(G) for m in range(M)]
         recv: Dict[tuple, Handle] = {}
         send_pending: Dict[int, SendHandle] = {}
@@ -149,11 +168,15 @@ class StageWorker:
             s, m = items[i]
             kb = recv_key_buf(s, m)
             if kb is not None and (s, m) not in recv:
-                recv[(s, m)] = self.t.irecv(kb[2], kb[1], kb[0])
+                # posted from m's lane: the comm stream then also waits for the
+                # previous reader of this buffer (microbatch m's last compute)
+                with on_lane(m):
+                    recv[(s, m)] = self.t.irecv(kb[2], kb[1], kb[0])
 
         def body(s, m, inp):
             """Compute of item (s, m); returns what goes downstream."""
             meta = pre_meta[m] if s == 0 else dec_meta[m]
+            st.backend.lane = m % L
             out = st.forward(meta, inp)
             if s > 0:
                 dec_meta[m].advance()
@@ -166,60 +189,23 @@ class StageWorker:
         t_start = time.perf_counter()
         post(0)
         for i, (s, m) in enumerate(items):
-            if spec.record_timing and m == 0 and self.device.type == "cuda":
-                ev = torch.cuda.Event(enable_timing=True)
-                ev.record()
-                step_events.append(ev)
-            # --- input
-            if (s, m) in recv:
-                inp = recv.pop((s, m)).wait()
-            elif self.first:
-                inp = prompt_ids[m] if s == 0 else tok_in[m]
-            else:
-                raise RuntimeError(f"stage {r}: no input posted for {(s, m)}")
-            if self.first and s > 0:
-                tok_out[m][s - 1].copy_(inp)
-            # Post the next receive before enqueueing this compute when it
-            # targets a different buffer (overlap); otherwise after.
-            cur_kb = recv_key_buf(s, m)
-            nxt_kb = recv_key_buf(*items[i + 1]) if i + 1 < len(items) else None
-            early = nxt_kb is not None and (cur_kb is None or nxt_kb[2] is not cur_kb[2])
-            if early:
-                post(i + 1)
-            # --- the previous send of this microbatch's static output must be done
-            if m in send_pending:
-                send_pending.pop(m).wait()
-            # --- compute
-            use_graph = spec.use_graphs and self.device.type == "cuda" and s >= 2
-            if use_graph:
-                if m not in graphs:
-                    graphs[m] = self._capture(lambda s=s, m=m, inp=inp: body(s, m, inp))
-                g, out = graphs[m]
-                g.replay()
-            else:
-                out = body(s, m, inp)
-            if not early:
-                post(i + 1)
-            # --- output
-            if self.last:
-                if P == 1:
-                    tok_in[m].copy_(out)
-                    if s == G - 1:
-                        tok_out[m][s].copy_(out)
-                else:
-                    send_pending[m] = self.t.send(out, 0, "ret")
-            else:
-                send_pending[m] = self.t.send(out, r + 1, "fwd")
+            with on_lane(m):
+                self._item(i, s, m, items, recv, send_pending, graphs, step_events, spec, post,
+                           recv_key_buf, body, prompt_ids, tok_in, tok_out, G, P, r)
         # Stage 0 still owes the receive of the final step's tokens.
         if self.first and P > 1:
             for m in range(M):
-                self.t.irecv(tok_in[m], P - 1, "ret").wait()
-                tok_out[m][G - 1].copy_(tok_in[m])
+                with on_lane(m):
+                    self.t.irecv(tok_in[m], P - 1, "ret").wait()
+                    tok_out[m][G - 1].copy_(tok_in[m])
         for h in send_pending.values():
             h.wait()
+        for lane in self.lanes:
+            torch.cuda.current_stream(dev).wait_stream(lane)
         if spec.record_timing and self.first and self.device.type == "cuda":
             ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
+            with on_lane(0):
+                ev.record()
             step_events.append(ev)
         self._sync()
         elapsed = (time.perf_counter() - t_start) * 1e3
@@ -233,6 +219,54 @@ class StageWorker:
         else:
             res.prefill_ms = elapsed
         return res
+
+    def _item(self, i, s, m, items, recv, send_pending, graphs, step_events, spec, post,
+              recv_key_buf, body, prompt_ids, tok_in, tok_out, G, P, r):
+        """One (step, microbatch) of the static schedule, on microbatch m's lane."""
+        if spec.record_timing and m == 0 and self.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            step_events.append(ev)
+        # --- input
+        if (s, m) in recv:
+            inp = recv.pop((s, m)).wait()
+        elif self.first:
+            inp = prompt_ids[m] if s == 0 else tok_in[m]
+        else:
+            raise RuntimeError(f"stage {r}: no input posted for {(s, m)}")
+        if self.first and s > 0:
+            tok_out[m][s - 1].copy_(inp)
+        # Post the next receive before enqueueing this compute when it
+        # targets a different buffer (overlap); otherwise after.
+        cur_kb = recv_key_buf(s, m)
+        nxt_kb = recv_key_buf(*items[i + 1]) if i + 1 < len(items) else None
+        early = nxt_kb is not None and (cur_kb is None or nxt_kb[2] is not cur_kb[2])
+        if early:
+            post(i + 1)
+        # --- the previous send of this microbatch's static output must be done
+        if m in send_pending:
+            send_pending.pop(m).wait()
+        # --- compute
+        use_graph = spec.use_graphs and self.device.type == "cuda" and s >= 2
+        if use_graph:
+            if m not in graphs:
+                graphs[m] = self._capture(lambda s=s, m=m, inp=inp: body(s, m, inp))
+            g, out = graphs[m]
+            g.replay()
+        else:
+            out = body(s, m, inp)
+        if not early:
+            post(i + 1)
+        # --- output
+        if self.last:
+            if P == 1:
+                tok_in[m].copy_(out)
+                if s == G - 1:
+                    tok_out[m][s].copy_(out)
+            else:
+                send_pending[m] = self.t.send(out, 0, "ret")
+        else:
+            send_pending[m] = self.t.send(out, r + 1, "fwd")
 
     # ------------------------------------------------------------------
     def _capture(self, fn):
