@@ -278,7 +278,8 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
     // Issue every slab load of a group before summing (no per-load branch:
     // clamped index x 0/1 mask), so the reduce is one round trip per group
     // instead of one per split.
-    constexpr int RG = (MT * NW <= 2) ? 8 : 4;
+    // group size: <= 128 VGPRs of in-flight partials (the W registers are dead here)
+    constexpr int RG = (32 / (MT * NW)) < 4 ? 4 : ((32 / (MT * NW)) > 16 ? 16 : 32 / (MT * NW));
     for (int s0 = 0; s0 < S; s0 += RG) {
       f32x4 v[RG][MT][NW];
 #pragma unroll

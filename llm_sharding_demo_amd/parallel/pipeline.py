@@ -37,6 +37,7 @@ import torch
 
 from ..models.stage import StageModel
 from ..runtime.batch import BatchMeta, SamplingState
+from ..utils.tracing import trace_range
 from .comm import Handle, SendHandle, Transport
 
 
@@ -189,7 +190,7 @@ class StageWorker:
         t_start = time.perf_counter()
         post(0)
         for i, (s, m) in enumerate(items):
-            with on_lane(m):
+            with on_lane(m), trace_range(f"stage{r}/step{s}/mb{m}"):
                 self._item(i, s, m, items, recv, send_pending, graphs, step_events, spec, post,
                            recv_key_buf, body, prompt_ids, tok_in, tok_out, G, P, r)
         # Stage 0 still owes the receive of the final step's tokens.

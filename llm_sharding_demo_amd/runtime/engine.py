@@ -100,7 +100,7 @@ class Engine:
             self.fabric = None
         else:
             raise ValueError(f"unknown mode {mode!r}")
-        self.slots = SlotAllocator(self.stages[0].kv.slots)
+        self.slots = _make_slot_allocator(self.stages[0].kv.slots)
 
     # ------------------------------------------------------------------
     def _build_stage(self, i: int, device: torch.device) -> StageModel:
@@ -259,6 +259,16 @@ class Engine:
         h = hidden.reshape(-1, self.mcfg.hidden).float()
         out = self._local_forward_range(h, 1, self.P, h.shape[0], True)
         return out[:, : self.mcfg.vocab_size]
+
+
+def _make_slot_allocator(n: int):
+    """Native (C++) KV-slot allocator when built, Python twin otherwise."""
+    from . import native
+
+    mod = native.load()
+    if mod is not None and os.environ.get("LSD_PY_RUNTIME", "0") != "1":
+        return mod.SlotAllocator(n)
+    return SlotAllocator(n)
 
 
 def build_engine(cfg: EngineConfig, **kw) -> Engine:
