@@ -183,14 +183,6 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
   for (int k0 = kb; k0 < ke; k0 += SK_ROUND_STEPS) {
     const int nst = min(SK_ROUND_STEPS, ke - k0);
     const int nch = (nst + 3) >> 2;
-    // A chunks: MT*4 wave-instructions (1 KiB = 4 rows of 256 B) per chunk
-    for (int inst = w; inst < nch * MT * 4; inst += 4) {
-      const int c = inst / (MT * 4), q = inst % (MT * 4);
-      const int row = q * 4 + (lane >> 4);
-      const int lch = (lane & 15) ^ (row & 15);
-      const int kk = min((k0 + c * 4) * 32 + lch * 8, p.K - 8);
-      glds16(p.A + (long)min(row, p.M - 1) * p.lda + kk, smem + c * CHUNK_BYTES + q * 1024);
-    }
     // All W fragments of the round are issued back to back.  No per-load guard:
     // a runtime "if (j < nst) load" makes hipcc branch around each load and
     // wait vmcnt(0) per element (guide §5 trap (c)); steps past the round end
@@ -200,6 +192,15 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
     for (int j = 0; j < SK_ROUND_STEPS; ++j)
 #pragma unroll
       for (int ns = 0; ns < NW; ++ns) wv[j][ns] = ld8(wrow[ns] + (long)(k0 + min(j, nst - 1)) * 32);
+    // A chunks (issued after W: the HBM-latency loads go first, the L2-resident
+    // activations overlap them): MT*4 wave-instructions (1 KiB = 4 rows of 256 B) per chunk
+    for (int inst = w; inst < nch * MT * 4; inst += 4) {
+      const int c = inst / (MT * 4), q = inst % (MT * 4);
+      const int row = q * 4 + (lane >> 4);
+      const int lch = (lane & 15) ^ (row & 15);
+      const int kk = min((k0 + c * 4) * 32 + lch * 8, p.K - 8);
+      glds16(p.A + (long)min(row, p.M - 1) * p.lda + kk, smem + c * CHUNK_BYTES + q * 1024);
+    }
     __syncthreads();  // vmcnt(0): the A image and this wave's W fragments have landed
     if (k0 == kb) { LSD_STAMP(1) }
     // A fragments come from LDS one step ahead of the MFMAs that use them, so
