@@ -17,6 +17,7 @@ using lsd::GemmParams;
 
 extern "C" {
 hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws, hipStream_t st);
+void lsd_gemm_set_big_min(int v);
 hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte, const bf16* wpe, float* out,
                      int T, int H, int vocab, hipStream_t st);
 hipError_t lsd_norm(float* x, const float* slab, int splits, const bf16* pbias, const bf16* w,
@@ -72,6 +73,7 @@ const bf16* opt_bias(const c10::optional<torch::Tensor>& b, int N) {
   if (!b.has_value()) return nullptr;
   need(*b, torch::kBFloat16, "bias");
   TORCH_CHECK(b->is_contiguous() && b->numel() == N, "bias must be contiguous [N]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(b->data_ptr()) % 16 == 0, "bias must be 16-byte aligned");
   return bptr(*b);
 }
 
@@ -168,6 +170,7 @@ c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
   need(x, torch::kFloat32, "x");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(0) == p.M && x.size(1) == p.N,
               "residual x must be contiguous [M, N]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "residual x must be 16-byte aligned");
   if (p.M == 0) return c10::nullopt;
   if (tiled && splits > 1) {
     TORCH_CHECK(splits <= p.K / 64, "splits must be <= K/64");
@@ -194,6 +197,8 @@ torch::Tensor linear_qkv(torch::Tensor a, torch::Tensor w, c10::optional<torch::
   need(vc, torch::kBFloat16, "v_cache");
   TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.sizes() == kc.sizes() && vc.is_contiguous(),
               "caches must be contiguous [slots, n_kv, max_seq, hd]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(kc.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(vc.data_ptr()) % 16 == 0, "caches must be 16-byte aligned");
   TORCH_CHECK(kc.size(3) == hd && kc.size(1) * hd == kv_size, "cache shape mismatch");
   TORCH_CHECK(p.N == q_size + 2 * kv_size, "w rows must be q_size + 2*kv_size");
   TORCH_CHECK(q_size % hd == 0 && hd % 16 == 0, "bad head dims");
@@ -299,6 +304,8 @@ void check_cache(const torch::Tensor& kc, const torch::Tensor& vc) {
   need(vc, torch::kBFloat16, "v_cache");
   TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && kc.sizes() == vc.sizes(),
               "caches must be contiguous [slots, n_kv, max_seq, hd]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(kc.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(vc.data_ptr()) % 16 == 0, "caches must be 16-byte aligned");
 }
 
 torch::Tensor attn_decode(torch::Tensor q, torch::Tensor kc, torch::Tensor vc,
@@ -392,5 +399,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample);
   m.def("set_stamps", &set_stamps);
+  // tiled GEMMs with >= this many 256x256 tiles use the pipelined 256^2 kernel
+  m.def("gemm_set_big_min", [](int64_t v) { lsd_gemm_set_big_min((int)v); });
   m.attr("arch") = "gfx950";
 }

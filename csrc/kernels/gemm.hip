@@ -119,6 +119,75 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int row0, int n, 
   }
 }
 
+// Row-contiguous epilogue of 8 consecutive columns [n, n+8) of row m (the
+// tiled kernel's LDS-transposed output): every store is one 16-byte vector.
+// n % 8 == 0; bias / out / x / caches are 16-byte aligned (host-checked).
+template <int EPI>
+__device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v,
+                                          int split) {
+  if constexpr (EPI == EPI_SLAB || EPI == EPI_F32) {
+    float* o = EPI == EPI_SLAB ? p.slab + (long)split * p.M * p.N + (long)m * p.N + n
+                               : reinterpret_cast<float*>(p.out) + (long)m * p.ldo + n;
+    reinterpret_cast<f32x4*>(o)[0] = f32x4{v[0], v[1], v[2], v[3]};
+    reinterpret_cast<f32x4*>(o)[1] = f32x4{v[4], v[5], v[6], v[7]};
+    return;
+  }
+  float y[8];
+  if (p.bias) {
+    const bf16x8 b = ld8(p.bias + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = v[j] + bf2f(b[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = v[j];
+  }
+  if constexpr (EPI == EPI_RESID) {
+    f32x4* x = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + (long)m * p.ldo + n);
+    f32x4 x0 = x[0], x1 = x[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { x0[j] += y[j]; x1[j] += y[4 + j]; }
+    x[0] = x0;
+    x[1] = x1;
+    return;
+  }
+  if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(EPI == EPI_GELU ? gelu_new(y[j]) : y[j]);
+    st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + n, o);
+    return;
+  }
+  if constexpr (EPI == EPI_QKV) {
+    const int qk = p.q_size + p.kv_size;
+    const int pos = p.tpos[m];
+    if (p.rope != nullptr && n < qk) {  // adjacent (even, odd) pairs rotate together
+      const int d0 = (n < p.q_size ? n : n - p.q_size) % p.hd;
+      const f32x4* cs = reinterpret_cast<const f32x4*>(p.rope + ((long)pos * (p.hd >> 1) + (d0 >> 1)) * 2);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 t = cs[h];  // (cos, sin) of pairs d0/2 + 2h, d0/2 + 2h + 1
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const float c = t[2 * e], s = t[2 * e + 1];
+          const float a = y[4 * h + 2 * e], b = y[4 * h + 2 * e + 1];
+          y[4 * h + 2 * e] = a * c - b * s;
+          y[4 * h + 2 * e + 1] = b * c + a * s;
+        }
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(y[j]);
+    if (n < p.q_size) {
+      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + n, o);
+    } else {
+      const int c = n < qk ? n - p.q_size : n - qk;
+      bf16* cache = n < qk ? p.kc : p.vc;
+      st8(cache + (((long)p.tslot[m] * p.n_kv + c / p.hd) * p.max_seq + pos) * p.hd + c % p.hd, o);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Decode GEMM (M <= 64): split-K across workgroups, last-arriver combine
 // ---------------------------------------------------------------------------
@@ -327,6 +396,8 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
 // ---------------------------------------------------------------------------
 constexpr int TBM = 128, TBN = 128, TBK = 64;
 constexpr int TILE_BYTES = TBM * TBK * 2;  // 16 KiB per operand tile
+constexpr int CT_LD = TBN + 4;              // epilogue fp32 C tile row stride (bank skew)
+constexpr int SMEM_TILED = TBM * CT_LD * 4 > 4 * TILE_BYTES ? TBM * CT_LD * 4 : 4 * TILE_BYTES;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void gbl_cvoid;
@@ -357,7 +428,7 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk)
 
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];  // [buf][A|W]
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_TILED];  // [buf][A|W]; then C tile
   const int nwg = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int per_split = tiles_m * tiles_n;
@@ -408,22 +479,241 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles
     cur ^= 1;
   }
 
+  // Epilogue through LDS (free after the loop's last barrier): the MFMA C
+  // layout gives each lane 4 rows x 1 column, i.e. 2-4-byte scattered stores;
+  // transposing the 128x128 fp32 tile through LDS turns every global store
+  // into a 16-byte row-contiguous vector (256 B per 16 lanes).
+  float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row0 = m0 + wm * 64 + i * 16 + 4 * g;
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        ct[(wm * 64 + i * 16 + 4 * g + q) * CT_LD + wn * 64 + j * 16 + r] = acc[i][j][q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < TBM * TBN / 8; c += 256) {
+    const int row = c >> 4, n = n0 + (c & 15) * 8, m = m0 + row;
+    if (m >= p.M || n >= p.N) continue;
+    const float* src = ct + row * CT_LD + (c & 15) * 8;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     if constexpr (EPI == EPI_SILU_MUL) {
+      // interleaved [gate16 | up16] 32-column blocks: gate chunks pair with
+      // the up chunk 16 columns right, in the same tile
+      if ((c & 3) >= 2) continue;
+      const float* up = src + 16;
+      const f32x4 ulo = *reinterpret_cast<const f32x4*>(up);
+      const f32x4 uhi = *reinterpret_cast<const f32x4*>(up + 4);
+      const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+      bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 4; j += 2) {
-        const int n = n0 + wn * 64 + j * 16 + r;
-        if (n < p.N) epilogue4<EPI>(p, row0, n, acc[i][j], acc[i][j + 1], split);
-      }
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
+      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
     } else {
+      epilogue8<EPI>(p, m, n, v, split);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Large GEMM (prefill, M >= 256): 256x256 tile, 8 waves (2 M x 4 N, 128x64
+// per wave), 4-slot LDS ring of BK=32 k-steps, fragments double-buffered in
+// registers across the barrier
+// ---------------------------------------------------------------------------
+// The 128x128 kernel above is the "two-barrier" structure: its __syncthreads
+// drains every LDS-DMA (vmcnt(0)) each k-step, and after each barrier every
+// wave stalls on its first ds_read before the MFMAs restart.  Here all LDS is
+// one array holding a ring of 4 slots of [256 rows][32 k] for A and W
+// (32 KiB per slot, 128 KiB, 1 block/CU).  Iteration s:
+//   * counted `s_waitcnt vmcnt(4|0)` retires this thread's glds of step s+1
+//     (step s+2's stay in flight), raw s_barrier publishes them to all waves;
+//   * glds of step s+3 into the slot step s-1 used (WAR-safe: that slot's
+//     fragments were read in iteration s-2 and consumed by MFMAs before this
+//     barrier);
+//   * 12 ds_read_b128 of step s+1's fragments into the idle register set;
+//   * 32 MFMAs of step s from the register set read one iteration earlier --
+//     they never wait on LDS, the reads above complete under them.
+// No other VMEM op sits in the loop, so the vmcnt counts are exact (guide §5
+// "Pipelining across barriers", traps 4(a)/(b)).
+//
+// LDS image per operand per slot: 64-B rows (32 k), the 16-B chunk index
+// XOR-swizzled by f((row >> 2) & 3), f = {0, 2, 3, 1}: with the ds_read_b128
+// lane groups of CDNA4 ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and +32)
+// every group of a fragment read covers 16 distinct 16-B bank slots.  glds
+// writes lane-linear, so the swizzle goes on the per-lane source address.
+constexpr int GBM = 256, GBN = 256, GBK = 32, GSLOTS = 4;
+constexpr int GOP_BYTES = GBM * GBK * 2;           // 16 KiB per operand per slot
+constexpr int GSLOT_BYTES = 2 * GOP_BYTES;         // A | W
+constexpr int GSMEM = GSLOTS * GSLOT_BYTES;        // 128 KiB (== 256 x 128 fp32 C half-tile)
+
+// s_waitcnt simm16 (gfx9 layout): vmcnt[3:0]+[15:14]=63, expcnt[6:4]=7, lgkmcnt[11:8]=0
+constexpr int LGKM0 = 0xC07F;
+
+__device__ __forceinline__ int big_swz(int q) { return (0x78 >> (2 * q)) & 3; }
+
+__device__ __forceinline__ void stage_big(char* lds, const bf16* src, long ld, int row0, int row_max,
+                                          int k0) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + r;
-        // N % 64 == 0 (host-checked): a whole 16-col tile is in or out, so the
-        // RoPE lane exchange never straddles the predicate.
-        if (n0 + wn * 64 + j * 16 < p.N) epilogue4<EPI>(p, row0, n, acc[i][j], acc[i][j], split);
+  for (int q = 0; q < 2; ++q) {
+    const int inst = w * 2 + q;                  // 16 instructions x 1 KiB = 16 rows x 64 B each
+    const int row = inst * 16 + (lane >> 2);
+    const int lch = (lane & 3) ^ big_swz((lane >> 4) & 3);  // (row >> 2) & 3 == (lane >> 4) & 3
+    const bf16* gp = src + (long)min(row0 + row, row_max) * ld + k0 + lch * 8;
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)gp, (lds_void*)(lds + inst * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 lds_frag_big(const char* op, int row, int g) {
+  return *reinterpret_cast<const bf16x8*>(op + row * 64 + ((g ^ big_swz((row >> 2) & 3)) << 4));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[GSMEM];
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int per_split = tiles_m * tiles_n;
+  const int split = bid / per_split;
+  const int t = bid % per_split;
+  const int tm = t % tiles_m, tn = t / tiles_m;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int KT = p.K / 64;  // split boundaries in 64-deep units: ns is even
+  const int kb = 2 * (int)((long)KT * split / p.splits);
+  const int ns = 2 * (int)((long)KT * (split + 1) / p.splits) - kb;
+
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int r = lane & 15, g = lane >> 4;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int step) {
+    char* slot = smem + (step & (GSLOTS - 1)) * GSLOT_BYTES;
+    const int k0 = (kb + step) * GBK;
+    stage_big(slot, p.A, p.lda, m0, p.M - 1, k0);
+    stage_big(slot + GOP_BYTES, p.W, p.ldw, n0, p.N - 1, k0);
+  };
+  auto frag_a = [&](int step, int i) {
+    return lds_frag_big(smem + (step & (GSLOTS - 1)) * GSLOT_BYTES, wr * 128 + i * 16 + r, g);
+  };
+  auto frag_w = [&](int step, int j) {
+    return lds_frag_big(smem + (step & (GSLOTS - 1)) * GSLOT_BYTES + GOP_BYTES, wc * 64 + j * 16 + r, g);
+  };
+  // wait for this thread's glds of `step`; steps after it stay in flight
+  auto wait_step = [&](int step) {
+    if (step + 1 < ns) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  // One k-step of MFMAs from (ac, wcur) while the next step's fragments are
+  // read into (an, wn): W and A rows 0-3 first, A rows 4-7 once the current
+  // A rows 0-3 are dead (keeps the live set at acc + 48 + 32 VGPRs).
+  auto step_mma = [&](int s, bf16x8 (&ac)[8], bf16x8 (&wcur)[4], bf16x8 (&an)[8], bf16x8 (&wn)[4]) {
+    // The next-step reads are unconditional (on the last step they read a
+    // stale slot and are discarded): a conditional register load would keep
+    // the old fragment set live through the loop and spill the accumulators.
+    if (s + 1 < ns) {
+      wait_step(s + 1);
+      if (s + 3 < ns) stage(s + 3);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wn[j] = frag_w(s + 1, j);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) an[i] = frag_a(s + 1, i);
+    // sched_barrier(0): keep the phase order as written -- hipcc otherwise
+    // hoists every read above the MFMAs and spills the accumulators
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(ac[i], wcur[j], acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) an[i] = frag_a(s + 1, i);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(ac[i], wcur[j], acc[i][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    // Retire the next set's reads (long done under the 32 MFMAs) with a real
+    // S_WAITCNT the waitcnt pass understands: the loop header then carries no
+    // pending LDS reads and the next step's MFMAs issue without the
+    // conservative lgkmcnt(0) hipcc otherwise puts in front of them.
+    __builtin_amdgcn_s_waitcnt(LGKM0);
+  };
+
+  bf16x8 a0[8], w0[4], a1[8], w1[4];
+  if (ns > 0) {
+#pragma unroll
+    for (int q = 0; q < GSLOTS - 1; ++q)
+      if (q < ns) stage(q);
+    // step 0 landed: steps 1, 2 may be in flight
+    if (ns >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ns == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w0[j] = frag_w(0, j);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a0[i] = frag_a(0, i);
+    __builtin_amdgcn_s_waitcnt(LGKM0);
+  }
+  // ns is even (splits partition K in 64-deep units): two steps per trip,
+  // the register sets swap roles without copies.
+  for (int s = 0; s < ns; s += 2) {
+    step_mma(s, a0, w0, a1, w1);
+    step_mma(s + 1, a1, w1, a0, w0);
+  }
+
+  // Epilogue: two passes over 128-column halves of the C tile, staged as fp32
+  // [256][128] in LDS (chunks of 16 floats XOR-swizzled by (row >> 2) & 3 so
+  // the MFMA-layout writes -- 4 rows x 16 columns per instruction -- hit
+  // distinct banks), then 16-byte row-contiguous epilogue8 stores.
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if ((wc >> 1) == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = wr * 128 + i * 16 + 4 * g + q;
+            const int col = (wc & 1) * 64 + j * 16 + r;
+            ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][q];
+          }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < GBM * 16; c += 512) {
+      const int row = c >> 4, ch = c & 15, m = m0 + row, n = n0 + h * 128 + ch * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const float* src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if constexpr (EPI == EPI_SILU_MUL) {
+        if ((ch & 3) >= 2) continue;  // up chunks are read by their gate chunk
+        const float* up = ct + row * 128 + (((ch + 2) * 8) ^ (((row >> 2) & 3) << 4));
+        const f32x4 ulo = *reinterpret_cast<const f32x4*>(up);
+        const f32x4 uhi = *reinterpret_cast<const f32x4*>(up + 4);
+        const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
+        st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
+      } else {
+        epilogue8<EPI>(p, m, n, v, split);
       }
     }
   }
@@ -432,6 +722,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
+static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
 template <int EPI>
 static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
   constexpr int NW = (EPI == EPI_SILU_MUL) ? 2 : 1;
@@ -449,6 +740,13 @@ static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_
 
 template <int EPI>
 static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
+  // 256x256 pipelined kernel once the problem fills the chip with 1-block/CU
+  // tiles; the 128x128 kernel (2 blocks/CU) for smaller M / N.
+  const int bm = (p.M + GBM - 1) / GBM, bn = (p.N + GBN - 1) / GBN;
+  if (p.M >= GBM && p.K % 64 == 0 && bm * bn * p.splits >= g_big_min_blocks) {
+    hipLaunchKernelGGL((gemm_big_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn);
+    return hipGetLastError();
+  }
   const int tm = (p.M + TBM - 1) / TBM, tn = (p.N + TBN - 1) / TBN;
   dim3 grid(tm * tn * p.splits), block(256);
   hipLaunchKernelGGL((gemm_tiled_kernel<EPI>), grid, block, 0, st, p, tm, tn);
@@ -458,6 +756,8 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
 }  // namespace lsd
 
 using namespace lsd;
+
+extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
 
 // C ABI used by csrc/bindings.cpp; shapes are validated there.
 extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws,

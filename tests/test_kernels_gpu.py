@@ -112,22 +112,65 @@ def test_gemm_large_prefill_shape(C, CNT):
     close(C.linear(a, w, None, 0, True, 1, CNT), ref.linear(a, w), 3e-2)
 
 
+@pytest.fixture
+def BIG(C):
+    """Force the pipelined 256x256 kernel for every tiled launch with M >= 256."""
+    C.gemm_set_big_min(1)
+    yield C
+    C.gemm_set_big_min(160)
+
+
+@pytest.mark.parametrize("M", [256, 300, 777])
+@pytest.mark.parametrize("K", [64, 128, 384])
+def test_big_gemm_epilogues(BIG, CNT, M, K):
+    """256x256 ring-pipelined kernel: every epilogue, M/N tails, K of 2, 4 and 12
+    k-steps (fewer than, equal to and more than the ring depth)."""
+    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
+
+    C = BIG
+    N = 320  # second column tile is a 64-wide tail
+    a, w, bias = bf(M, K, seed=40), bf(N, K, scale=0.05, seed=41), bf(N, scale=0.1, seed=42)
+    y_ref = ref.linear(a, w, bias)
+    close(C.linear(a, w, bias, 0, True, 1, CNT), y_ref, 3e-2)
+    close(C.linear(a, w, bias, 1, True, 1, CNT), ref.gelu_new(y_ref), 3e-2)
+    w2 = w[:256].contiguous()
+    y = C.linear(a, interleave_gate_up(w2, 128).contiguous(), None, 2, True, 1, CNT)
+    close(y, ref.silu_mul(*ref.linear(a, w2).split(128, 1)), 3e-2)
+    close(C.linear_f32(a, w, True, 1, CNT), ref.linear(a, w), 2e-3, 1e-3)
+    x = torch.randn(M, N, device=DEV)
+    x_ref = x + y_ref
+    assert C.linear_residual(a, w, bias, x, 1, True, CNT) is None
+    close(x, x_ref, 2e-3, 1e-3)
+    if K >= 128:
+        x = torch.randn(M, N, device=DEV)
+        x_ref = x + y_ref
+        slab = C.linear_residual(a, w, bias, x, 2, True, CNT)
+        C.norm(x, slab, bias, None, None, 0.0, True, None, False)
+        close(x, x_ref, 2e-3, 1e-3)
+
+
 def _cache(slots, n_kv, S, hd):
     return (torch.zeros(slots, n_kv, S, hd, dtype=torch.bfloat16, device=DEV),
             torch.zeros(slots, n_kv, S, hd, dtype=torch.bfloat16, device=DEV))
 
 
 @pytest.mark.parametrize("rope", [False, True])
-@pytest.mark.parametrize("splits", [1, 4])
-def test_qkv_kv_append(C, CNT, rope, splits):
+@pytest.mark.parametrize("mode", ["decode1", "decode4", "tiled", "big"])
+def test_qkv_kv_append(C, CNT, rope, mode):
     from llm_sharding_demo_amd.ops.hip import rope_pair_permutation, rope_table
 
     nh, n_kv, hd, H = 4, 2, 64, 256
     qs, kvs = nh * hd, n_kv * hd
-    T, slots, S = 10, 3, 32
+    tiled = mode in ("tiled", "big")
+    splits = 4 if mode == "decode4" else 1
+    # decode: 10 tokens of 2 sequences; tiled: 2 sequences of 150 tokens
+    n0, n1 = (4, 6) if not tiled else (150, 150)
+    T, slots, S = n0 + n1, 3, 320
     a, w, bias = bf(T, H, seed=13), bf(qs + 2 * kvs, H, scale=0.05, seed=14), bf(qs + 2 * kvs, scale=0.1, seed=15)
-    tslot = torch.tensor([0] * 4 + [2] * 6, dtype=torch.int32, device=DEV)
-    tpos = torch.tensor(list(range(4)) + list(range(5, 11)), dtype=torch.int32, device=DEV)
+    tslot = torch.tensor([0] * n0 + [2] * n1, dtype=torch.int32, device=DEV)
+    tpos = torch.tensor(list(range(n0)) + list(range(5, 5 + n1)), dtype=torch.int32, device=DEV)
+    if mode == "big":
+        C.gemm_set_big_min(1)
     kc, vc = _cache(slots, n_kv, S, hd)
     kr, vr = _cache(slots, n_kv, S, hd)
     y = ref.linear(a, w, bias)
@@ -141,14 +184,15 @@ def test_qkv_kv_append(C, CNT, rope, splits):
                           torch.arange(qs + kvs, qs + 2 * kvs)]).to(DEV)
         w, bias = w[perm].contiguous(), bias[perm].contiguous()
         table = rope_table(S, hd, 10000.0, DEV)
-        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, table, False, splits, CNT)
+        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, table, tiled, splits, CNT)
         # un-permute the pair-interleaved head dims for comparison
         p1 = rope_pair_permutation(1, hd)
         inv = torch.argsort(p1).to(DEV)
         q = q.reshape(T, nh, hd)[:, :, inv]
         kc = kc[..., inv]
     else:
-        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, None, False, splits, CNT).reshape(T, nh, hd)
+        q = C.linear_qkv(a, w, bias, kc, vc, tslot, tpos, qs, kvs, hd, None, tiled, splits, CNT).reshape(T, nh, hd)
+    C.gemm_set_big_min(160)
     ref.kv_append(kr, vr, k_ref, v_ref, tslot, tpos)
     close(q, q_ref, 3e-2)
     close(kc, kr, 3e-2)

@@ -101,6 +101,46 @@ def bench_gemm(M, N, K, act=0, resid=False, label=""):
     report(f"gemm{label} M={M} N={N} K={K} S={splits}", us, N * K * 2, {"hipblaslt_us": round(ut, 2)})
 
 
+def bench_prefill_gemms(T, H, F, nh, hd, label=""):
+    """Prefill-shaped tiled GEMMs with their real fused epilogues (QKV scatter
+    into the KV cache, bias+GELU, residual add) vs plain hipBLASLt matmul."""
+    nseq = T // 128
+    kc = torch.zeros(nseq, nh, 128, hd, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    slot = torch.arange(nseq, dtype=torch.int32, device=DEV).repeat_interleave(128)
+    pos = torch.arange(128, dtype=torch.int32, device=DEV).repeat(nseq)
+    a = torch.randn(T, H, device=DEV).bfloat16()
+    af = torch.randn(T, F, device=DEV).bfloat16()
+    x = torch.randn(T, H, device=DEV)
+    wq = torch.randn(3 * H, H, device=DEV).bfloat16()
+    bq = torch.randn(3 * H, device=DEV).bfloat16()
+    wf = torch.randn(F, H, device=DEV).bfloat16()
+    bf = torch.randn(F, device=DEV).bfloat16()
+    wp = torch.randn(H, H, device=DEV).bfloat16()
+    wp2 = torch.randn(H, F, device=DEV).bfloat16()
+    cases = [
+        ("qkv", lambda: C.linear_qkv(a, wq, bq, kc, vc, slot, pos, H, H, hd, None, True, 1, None),
+         lambda: torch.matmul(a, wq.t()), 3 * H, H),
+        ("fc_gelu", lambda: C.linear(a, wf, bf, 1, True, 1, None), lambda: torch.matmul(a, wf.t()), F, H),
+        ("proj_resid", lambda: C.linear_residual(a, wp, None, x, 1, True, None),
+         lambda: torch.matmul(a, wp.t()), H, H),
+        ("proj2_resid", lambda: C.linear_residual(af, wp2, None, x, 1, True, None),
+         lambda: torch.matmul(af, wp2.t()), H, F),
+    ]
+    for name, fn, ref, N, K in cases:
+        C.gemm_set_big_min(1 << 30)
+        u128 = timeit(fn, iters=20)
+        C.gemm_set_big_min(1)
+        us = timeit(fn, iters=20)
+        C.gemm_set_big_min(160)
+        ut = timeit(ref, iters=20)
+        fl = 2.0 * T * N * K
+        report(f"prefill{label}_{name} M={T} N={N} K={K}", us, 0,
+               {"TFLOP/s": round(fl / us / 1e6, 1), "tile128_us": round(u128, 2),
+                "tile128_TFLOP/s": round(fl / u128 / 1e6, 1), "hipblaslt_us": round(ut, 2),
+                "hipblaslt_TFLOP/s": round(fl / ut / 1e6, 1)})
+
+
 def bench_attn_decode(B, nh, n_kv, hd, ctx, slots=None):
     slots = slots or B
     S = ctx + 1
@@ -213,6 +253,9 @@ def main():
         for M in (1, 64):
             bench_gemm(M, V, H, act=0, label="_lmhead")
         bench_gemm(8192, 3 * H, H, label="_prefill_qkv")
+    if "prefill" in which:
+        bench_prefill_gemms(8192, H, F, 25, 64)
+        bench_prefill_gemms(4096, 4096, 14336, 32, 128, label="_llama")
     if "attn" in which:
         for B in (1, 16, 64):
             bench_attn_decode(B, 25, 25, 64, 192)
