@@ -18,6 +18,7 @@ using lsd::GemmParams;
 extern "C" {
 hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws, hipStream_t st);
 void lsd_gemm_set_big_min(int v);
+int lsd_gemm_sk_rows(int M);
 hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte, const bf16* wpe, float* out,
                      int T, int H, int vocab, hipStream_t st);
 hipError_t lsd_norm(float* x, const float* slab, int splits, const bf16* pbias, const bf16* w,
@@ -92,7 +93,7 @@ GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, bool tile
   if (tiled) {
     TORCH_CHECK(p.K % 64 == 0, "tiled GEMM needs K % 64 == 0, got ", p.K);
   } else {
-    TORCH_CHECK(p.M >= 1 && p.M <= 64, "decode GEMM needs 1 <= M <= 64, got ", p.M);
+    TORCH_CHECK(p.M >= 1 && p.M <= 128, "decode GEMM needs 1 <= M <= 128, got ", p.M);
     TORCH_CHECK(p.K % 32 == 0, "decode GEMM needs K % 32 == 0, got ", p.K);
     TORCH_CHECK(p.N % 64 == 0, "decode GEMM needs N % 64 == 0 (pad the weight), got ", p.N);
   }
@@ -120,7 +121,7 @@ void run_gemm(GemmParams& p, int epi, bool tiled, int64_t splits,
       TORCH_CHECK(counters->is_contiguous() && counters->numel() >= tiles,
                   what, ": counter buffer too small (", counters->numel(), " < ", tiles, ")");
       cnt = counters->data_ptr<int>();
-      const long rows = ((p.M + 15) / 16) * 16;
+      const long rows = lsd_gemm_sk_rows(p.M);  // rows of the launched row tile
       const long bytes = tiles * splits * rows * 64 * nw * 4;
       TORCH_CHECK(splits * rows * 64 * nw * 4 < (1L << 31), what, ": split workspace too large");
       wsbuf = torch::empty({bytes / 4}, like.options().dtype(torch::kFloat32));

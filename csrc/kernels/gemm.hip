@@ -189,11 +189,11 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 }
 
 // ---------------------------------------------------------------------------
-// Decode GEMM (M <= 64): split-K across workgroups, last-arriver combine
+// Decode GEMM (M <= 128): split-K across workgroups, last-arriver combine
 // ---------------------------------------------------------------------------
 // grid = (N / (64*NW) column tiles, S k-splits); block = 4 waves, wave w owns
 // columns [16*NW*w, 16*NW*(w+1)) of the block's tile and the whole K range of
-// the split.  Per round of up to 512 k:
+// the split.  Per round of up to 512 k (256 k for M > 64):
 //   * A[0:M, k-range] -> LDS with 16-B LDS-DMA (global_load_lds), whole 128-B
 //     lines per instruction (not 16-row fragment-shaped loads, which double
 //     TA traffic: guide §5 "x operand through LDS in full lines"), one image of
@@ -206,7 +206,10 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 // release/acquire ticket, guide §5 "In-launch split-K reduction") sums the S
 // partials and runs the fused epilogue -- so any epilogue (QKV scatter + RoPE,
 // GELU, residual add) works with any split and no extra launch is needed.
-constexpr int SK_ROUND_STEPS = 16;  // 32-k MFMA steps per round (512 k)
+// 32-k MFMA steps per round: 16 (512 k) up to M = 64; 8 (256 k) for M <= 128
+// so the A image stays at 64 KiB (2 blocks / CU) while the rows double.
+template <int MT>
+constexpr int sk_round_steps() { return MT > 4 ? 8 : 16; }
 
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)g,
@@ -225,8 +228,10 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
   constexpr int ROWS = MT * 16;
   constexpr int CHUNK_BYTES = ROWS * 256;  // one [ROWS][128 k] bf16 image
   constexpr int BNB = 64 * NW;             // block tile columns
-  __shared__ __attribute__((aligned(16))) char smem[4 * CHUNK_BYTES + 16];
-  int* s_flag = reinterpret_cast<int*>(smem + 4 * CHUNK_BYTES);
+  constexpr int SK_ROUND_STEPS = sk_round_steps<MT>();
+  constexpr int NCHUNK = SK_ROUND_STEPS / 4;
+  __shared__ __attribute__((aligned(16))) char smem[NCHUNK * CHUNK_BYTES + 16];
+  int* s_flag = reinterpret_cast<int*>(smem + NCHUNK * CHUNK_BYTES);
 
   LSD_STAMP(0)
   if (p.stamps && threadIdx.x == 0)
@@ -723,16 +728,26 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m
 // Host launchers
 // ---------------------------------------------------------------------------
 static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
+// Row tiles (16 rows each) of the decode kernel launched for M rows: MT is
+// instantiated for {1, 2, 3, 4, 6, 8}.  The split-K workspace is sized from
+// this (lsd_gemm_sk_rows), so the two can never disagree.
+static int sk_mt(int M) {
+  const int mt = (M + 15) / 16;
+  return mt == 5 || mt == 7 ? mt + 1 : mt;
+}
+
 template <int EPI>
 static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
   constexpr int NW = (EPI == EPI_SILU_MUL) ? 2 : 1;
-  const int MT = (p.M + 15) / 16;
+  const int MT = sk_mt(p.M);
   dim3 grid(p.N / (64 * NW), p.splits), block(256);
   switch (MT) {
     case 1: hipLaunchKernelGGL((gemm_sk_kernel<1, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
     case 2: hipLaunchKernelGGL((gemm_sk_kernel<2, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
     case 3: hipLaunchKernelGGL((gemm_sk_kernel<3, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
     case 4: hipLaunchKernelGGL((gemm_sk_kernel<4, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
+    case 6: hipLaunchKernelGGL((gemm_sk_kernel<6, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
+    case 8: hipLaunchKernelGGL((gemm_sk_kernel<8, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -758,6 +773,7 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
 using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
+extern "C" int lsd_gemm_sk_rows(int M) { return sk_mt(M) * 16; }
 
 // C ABI used by csrc/bindings.cpp; shapes are validated there.
 extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws,

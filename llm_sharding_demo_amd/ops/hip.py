@@ -82,6 +82,8 @@ class HipBackend(Backend):
     name = "hip"
     TARGET_BLOCKS = 512  # >> 256 CUs so every CU streams
     # decode GEMM: aim for this many workgroups (column tiles x k-splits)
+    # decode (split-K, last-arriver) GEMM up to this many rows; tiled above
+    SK_MAX_M = int(os.environ.get("LSD_SK_MAX_M", "128"))
     SK_TARGET = int(os.environ.get("LSD_SK_TARGET", "384"))
     SK_MIN_STEPS = int(os.environ.get("LSD_SK_MIN_STEPS", "2"))  # 32-k steps per split
 
@@ -126,9 +128,9 @@ class HipBackend(Backend):
         self._counters = None if value is None else value.reshape(-1, 1 << 16)
 
     # ------------------------------------------------------------------
-    @staticmethod
-    def _tiled(M: int) -> bool:
-        return M > 64
+    @classmethod
+    def _tiled(cls, M: int) -> bool:
+        return M > cls.SK_MAX_M
 
     def _resid_splits(self, M: int, N: int, K: int) -> int:
         if self._tiled(M):

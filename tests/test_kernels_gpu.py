@@ -61,7 +61,7 @@ def CNT():
     return torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 65, 200])
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 65, 100, 128, 200])
 @pytest.mark.parametrize("act", ["none", "gelu", "silu_mul"])
 @pytest.mark.parametrize("splits", [1, 3, 7])
 def test_linear(C, CNT, M, act, splits):
@@ -69,7 +69,7 @@ def test_linear(C, CNT, M, act, splits):
 
     N, K = 384, 640
     a, w, bias = bf(M, K, seed=5), bf(N, K, scale=0.05, seed=6), bf(N, scale=0.1, seed=7)
-    tiled = M > 64
+    tiled = M > 128
     sp = 1 if tiled else splits
     if act == "silu_mul":
         N = 256
@@ -85,11 +85,11 @@ def test_linear(C, CNT, M, act, splits):
     assert int(CNT.abs().sum()) == 0  # every ticket counter re-armed
 
 
-@pytest.mark.parametrize("M,splits", [(3, 1), (16, 4), (64, 5), (64, 16), (100, 1), (130, 3)])
+@pytest.mark.parametrize("M,splits", [(3, 1), (16, 4), (64, 5), (64, 16), (100, 1), (128, 5), (130, 3)])
 def test_linear_residual_and_f32(C, CNT, M, splits):
     N, K = 256, 1024
     a, w, bias = bf(M, K, seed=8), bf(N, K, scale=0.05, seed=9), bf(N, scale=0.1, seed=10)
-    tiled = M > 64
+    tiled = M > 128
     x = torch.randn(M, N, device=DEV)
     x_ref = x + ref.linear(a, w, bias)
     slab = C.linear_residual(a, w, bias, x, splits, tiled, CNT)
