@@ -6,7 +6,8 @@ One step = one complete generation round, end to end: prefill of every
 prompt, then `--gen` decode steps, for a global batch of N x --batch
 sequences split into 2N microbatches that flow through the N-stage pipeline
 (one stage per GPU, RCCL p2p between stages; each stage keeps two
-microbatches in flight on two HIP streams).  Weak scaling: each GPU holds
+microbatches in flight on two HIP streams).  `--dp R` instead runs R
+replicas of an N/R-stage pipeline (hybrid PP x DP).  Weak scaling: each GPU holds
 1/N of the layers and the global batch grows with N.  Nothing is skipped in
 the timed region: prefill, every layer, lm_head and the sampler (reference
 sampler: T=0.6, top-k=40; --greedy for argmax) run for every token.
@@ -43,8 +44,12 @@ def parse():
     p.add_argument("--gen", type=int, default=128)
     p.add_argument("--microbatches", type=int, default=int(os.environ.get("BENCH_MB", "0")),
                    help="0 -> 2N: two 64-sequence microbatches in flight per stage")
+    p.add_argument("--dp", type=int, default=int(os.environ.get("BENCH_DP", "1")),
+                   help="pipeline replicas: N GPUs = (N/dp)-stage pipeline x dp (default 1: ppN)")
     p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),
                    help="nccl (RCCL over xGMI) | gloo (host-staged, for rehearsals)")
+    p.add_argument("--device", default="cuda",
+                   help="cuda (MI355X); cpu only to rehearse the multi-rank contract with gloo")
     p.add_argument("--greedy", action="store_true")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--seed", type=int, default=0)
@@ -62,44 +67,57 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != N:
         raise SystemExit(f"--gpus {N} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    M = args.microbatches or 2 * N
-    B = N * args.batch
-    cfg = EngineConfig(model_id=args.model, num_stages=N, max_batch=B,
-                       max_seq_len=args.prompt + args.gen, device="cuda",
+    R = args.dp
+    if N % R:
+        raise SystemExit(f"--gpus {N} is not a multiple of --dp {R}")
+    P = N // R                      # pipeline stages per replica
+    M = args.microbatches or 2 * P  # microbatches per replica
+    B = N * args.batch              # global batch (weak scaling: fixed per GPU)
+    Br = P * args.batch             # sequences per replica
+    cfg = EngineConfig(model_id=args.model, num_stages=P, dp_replicas=R, max_batch=Br,
+                       max_seq_len=args.prompt + args.gen, device=args.device,
                        use_graphs=not args.no_graphs, num_microbatches=M, seed=args.seed,
                        transport=args.transport)
     eng = Engine(cfg, mode="dist" if N > 1 else "local")
     rank = eng.rank
     worker = eng.workers[0]
 
-    rnd = random.Random(args.seed)
     vocab = cfg.model.vocab_size
-    prompts = [[rnd.randrange(vocab) for _ in range(args.prompt)] for _ in range(B)]
     sp = SamplingParams(greedy=args.greedy, temperature=0.6, top_k=40,
                         max_new_tokens=args.gen, seed=1234)
-    slots = list(range(B))
-    # every rank builds the identical round spec (deterministic), no broadcast
-    eng._rng = random.Random(args.seed)
-    spec = eng.make_round(prompts, [sp] * B, slots, microbatches=M, record_timing=(rank == 0))
+    # every rank builds the identical per-replica round specs (deterministic),
+    # no broadcast; each rank runs its own replica's
+    specs = []
+    for rep in range(R):
+        rnd = random.Random(args.seed * 1000 + rep)
+        prompts = [[rnd.randrange(vocab) for _ in range(args.prompt)] for _ in range(Br)]
+        eng._rng = random.Random(args.seed * 1000 + rep)
+        specs.append(eng.make_round(prompts, [sp] * Br, list(range(Br)), microbatches=M,
+                                    record_timing=(rank == 0)))
+    spec = specs[eng.replica]
 
     def barrier():
         if N > 1:
             eng.transport.barrier()
 
+    def sync():
+        if args.device != "cpu":
+            torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         worker.run_round(spec)
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     step_ms = []
     for _ in range(args.steps):
         res = worker.run_round(spec)
         if rank == 0 and res is not None:
             step_ms += res.step_times_ms
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     if N > 1:
         import torch.distributed as dist
@@ -119,11 +137,13 @@ def main() -> int:
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / base, 1) if base else None,
-            "dtype": "bf16", "data": "synthetic prompts, random-init weights",
+            "dtype": "bf16" if args.device != "cpu" else "fp32",
+            "data": "synthetic prompts, random-init weights",
             "p50_token_latency_ms": round(p50, 4) if p50 is not None else None,
             "config": {"model": args.model, "global_batch": B, "seq_len": args.prompt + args.gen,
                        "prompt_len": args.prompt, "gen_tokens": args.gen, "microbatches": M,
-                       "parallelism": f"pp{N}", "sampler": "greedy" if args.greedy else "T0.6/top-k40",
+                       "parallelism": f"pp{P}" + (f"xdp{R}" if R > 1 else ""),
+                       "sampler": "greedy" if args.greedy else "T0.6/top-k40",
                        "hipgraphs": not args.no_graphs},
         }
         print(json.dumps(out), flush=True)

@@ -206,6 +206,10 @@ class EngineConfig:
     model_id: str = "sshleifer/tiny-gpt2"
     # Pipeline: number of stages (= GPUs, one rank per GPU) and the layer split.
     num_stages: int = 1
+    # Data parallelism over whole pipelines: world = num_stages x dp_replicas
+    # ranks; replica r owns ranks [r*P, (r+1)*P).  Requests are spread over
+    # the replicas (SURVEY.md §2.2 "DP -- request-level replicas").
+    dp_replicas: int = 1
     # Explicit split points (len num_stages-1), e.g. SPLIT_AT=2 -> [2].  None = cost model.
     split_points: Optional[Sequence[int]] = None
     dtype: str = "bf16"  # compute / storage dtype on GPU; CPU golden runs in fp32
@@ -245,6 +249,7 @@ class EngineConfig:
             dtype=_env("DTYPE", "bf16"),
             weights=os.environ.get("WEIGHTS") or None,
             transport=_env("TRANSPORT", "auto"),
+            dp_replicas=int(_env("DP_REPLICAS", "1") or 1),
         )
         if cfg.split_points and cfg.num_stages == 1:
             cfg.num_stages = len(cfg.split_points) + 1

@@ -94,30 +94,50 @@ class Transport:
 # ---------------------------------------------------------------------------
 
 class _DistTransport(Transport):
-    def __init__(self, num_stages: int):
+    """Ranks are laid out replica-major: global rank = replica * P + stage.
+    `send`/`irecv` address peers by STAGE index inside this rank's replica;
+    every replica has its own per-edge communicators, so replicas never
+    share a link or an RCCL stream."""
+
+    def __init__(self, num_stages: int, replicas: int = 1):
         import torch.distributed as dist
 
         self.dist = dist
-        self.rank = dist.get_rank()
-        self.world = dist.get_world_size()
-        if self.world != num_stages:
-            raise TransportError(f"world size {self.world} != num_stages {num_stages}")
+        self.grank = dist.get_rank()
+        self.gworld = dist.get_world_size()
+        P, R = num_stages, replicas
+        if self.gworld != P * R:
+            raise TransportError(f"world size {self.gworld} != num_stages {P} x replicas {R}")
+        self.P, self.R = P, R
+        self.replica, self.rank = divmod(self.grank, P)  # rank = stage index
+        self.world = P
         # Groups must be created by every rank in the same order.
         self.groups: Dict[str, object] = {}
-        P = num_stages
-        for i in range(P - 1):
-            self.groups[f"fwd{i}"] = dist.new_group([i, i + 1], backend=self._backend())
-        if P > 1:
-            self.groups["ret"] = dist.new_group([P - 1, 0], backend=self._backend())
-        self.ctrl = dist.new_group(list(range(P)), backend="gloo")
+        for rep in range(R):
+            base = rep * P
+            for i in range(P - 1):
+                self.groups[f"r{rep}fwd{i}"] = dist.new_group([base + i, base + i + 1],
+                                                              backend=self._backend())
+            if P > 1:
+                self.groups[f"r{rep}ret"] = dist.new_group([base + P - 1, base], backend=self._backend())
+        self.ctrl = dist.new_group(list(range(P * R)), backend="gloo")
 
     def _backend(self) -> str:
         raise NotImplementedError
 
+    def _g(self, stage: int) -> int:
+        return self.replica * self.P + stage
+
     def _edge_group(self, edge: str, src: int, dst: int):
         if edge == "fwd":
-            return self.groups[f"fwd{min(src, dst)}"]
-        return self.groups["ret"]
+            return self.groups[f"r{self.replica}fwd{min(src, dst)}"]
+        return self.groups[f"r{self.replica}ret"]
+
+    def gather_object(self, obj, dst: int = 0):
+        """Gather one picklable object per rank on global rank `dst` (ctrl plane)."""
+        out = [None] * self.gworld if self.grank == dst else None
+        self.dist.gather_object(obj, out, dst=dst, group=self.ctrl)
+        return out
 
     def broadcast_object(self, obj, src: int = 0):
         lst = [obj]
@@ -139,26 +159,28 @@ class NcclTransport(_DistTransport):
         rank blocks in a lazy ncclCommInitRank while its peer waits elsewhere."""
         dev = torch.device(device)
         for name, g in self.groups.items():
-            members = self._members(name)
-            if self.rank in members:
+            if self.grank in self._members(name):
                 t = torch.ones(1, device=dev)
                 self.dist.all_reduce(t, group=g)
         torch.cuda.synchronize(dev)
         self.barrier()
 
     def _members(self, name: str) -> List[int]:
-        if name == "ret":
-            return [self.world - 1, 0]
-        i = int(name[3:])
-        return [i, i + 1]
+        """Global ranks of group `r{rep}fwd{i}` / `r{rep}ret`."""
+        rep, kind = name[1:].split("fwd") if "fwd" in name else (name[1:-3], "ret")
+        base = int(rep) * self.P
+        if kind == "ret":
+            return [base + self.P - 1, base]
+        i = int(kind)
+        return [base + i, base + i + 1]
 
     def send(self, t, dst, edge):
         g = self._edge_group(edge, self.rank, dst)
-        return SendHandle(self.dist.isend(t, dst, group=g))
+        return SendHandle(self.dist.isend(t, self._g(dst), group=g))
 
     def irecv(self, out, src, edge):
         g = self._edge_group(edge, src, self.rank)
-        return Handle(out, self.dist.irecv(out, src, group=g))
+        return Handle(out, self.dist.irecv(out, self._g(src), group=g))
 
 
 class GlooTransport(_DistTransport):
@@ -170,14 +192,14 @@ class GlooTransport(_DistTransport):
     def send(self, t, dst, edge):
         g = self._edge_group(edge, self.rank, dst)
         host = t.detach().to("cpu", copy=True) if t.device.type != "cpu" else t.detach().clone()
-        return SendHandle(self.dist.isend(host, dst, group=g))
+        return SendHandle(self.dist.isend(host, self._g(dst), group=g))
 
     def irecv(self, out, src, edge):
         g = self._edge_group(edge, src, self.rank)
         if out.device.type == "cpu":
-            return Handle(out, self.dist.irecv(out, src, group=g))
+            return Handle(out, self.dist.irecv(out, self._g(src), group=g))
         host = torch.empty(out.shape, dtype=out.dtype)
-        work = self.dist.irecv(host, src, group=g)
+        work = self.dist.irecv(host, self._g(src), group=g)
         return Handle(out, work, post=lambda: out.copy_(host))
 
 
@@ -281,13 +303,13 @@ def init_distributed(backend: str, device_type: str) -> None:
     dist.init_process_group(backend=backend, **kw)
 
 
-def make_dist_transport(num_stages: int, kind: str, device) -> Transport:
+def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1) -> Transport:
     if kind == "nccl":
-        t = NcclTransport(num_stages)
+        t = NcclTransport(num_stages, replicas)
         t.warmup(device)
         return t
     if kind == "gloo":
-        t = GlooTransport(num_stages)
+        t = GlooTransport(num_stages, replicas)
         t.barrier()
         return t
     raise ValueError(f"unknown transport {kind!r}")

@@ -9,10 +9,12 @@ Execution modes
               runs one thread per stage over the in-memory LocalTransport
               (each stage may sit on its own device).  Used on CPU (tests)
               and for single-GPU runs.
-  * dist   -- one process per MI355X under torchrun; rank r owns stage r.
-              Rank 0 is the coordinator and also stage 0; other ranks sit in
-              `worker_loop()` and receive round specs over a gloo control
-              group.  Data moves over RCCL p2p (NcclTransport).
+  * dist   -- one process per MI355X under torchrun; rank r owns stage
+              r % P of pipeline replica r // P (dp_replicas R, world = P*R).
+              Rank 0 is the coordinator and also stage 0 of replica 0; other
+              ranks sit in `worker_loop()` and receive per-replica round specs
+              over a gloo control group.  Data moves over RCCL p2p
+              (NcclTransport), one set of edge communicators per replica.
 """
 from __future__ import annotations
 
@@ -61,6 +63,10 @@ class Engine:
         self.mcfg = cfg.model
         self.mode = mode
         self.P = cfg.num_stages
+        self.R = max(1, cfg.dp_replicas)
+        if mode == "local" and self.R != 1:
+            raise ValueError("dp_replicas > 1 needs the dist mode (one process per GPU)")
+        self.replica, self.stage_idx = 0, 0
         self.plan = make_plan(self.mcfg, self.P, cfg.split_points, batch=cfg.max_batch,
                               avg_ctx=min(256, cfg.max_seq_len))
         self._rng = random.Random(cfg.seed)
@@ -93,14 +99,17 @@ class Engine:
             if dev.type == "cuda":
                 dev = torch.device("cuda", torch.cuda.current_device())
             self.devices = [dev]
-            self.transport = make_dist_transport(self.P, kind, dev)
-            stage = self._build_stage(self.rank, dev)
+            self.transport = make_dist_transport(self.P, kind, dev, self.R)
+            self.replica, self.stage_idx = self.transport.replica, self.transport.rank
+            stage = self._build_stage(self.stage_idx, dev)
             self.stages = [stage]
-            self.workers = [StageWorker(stage, self.transport, self.rank, self.P)]
+            self.workers = [StageWorker(stage, self.transport, self.stage_idx, self.P)]
             self.fabric = None
         else:
             raise ValueError(f"unknown mode {mode!r}")
-        self.slots = _make_slot_allocator(self.stages[0].kv.slots)
+        # one KV-slot pool per pipeline replica (the coordinator allocates for all)
+        self.slot_pools = [_make_slot_allocator(self.stages[0].kv.slots) for _ in range(self.R)]
+        self.slots = self.slot_pools[0]
 
     # ------------------------------------------------------------------
     def _build_stage(self, i: int, device: torch.device) -> StageModel:
@@ -115,10 +124,25 @@ class Engine:
         return self.rank == 0
 
     # ------------------------------------------------------------------
+    def _run_rounds(self, specs: List[Optional[RoundSpec]]) -> List[Optional[RoundResult]]:
+        """One round per pipeline replica (None = replica idle this round)."""
+        if self.mode != "dist":
+            return [self._run_round(specs[0])]
+        self.transport.broadcast_object(("round", specs), src=0)
+        return self._dist_round(specs)
+
+    def _dist_round(self, specs) -> List[Optional[RoundResult]]:
+        spec = specs[self.replica]
+        res = self.workers[0].run_round(spec) if spec is not None else None
+        if self.R == 1:
+            return [res]
+        # stage 0 of every replica holds its replica's tokens; collect on rank 0
+        got = self.transport.gather_object(res if self.stage_idx == 0 else None, dst=0)
+        return None if got is None else [got[r * self.P] for r in range(self.R)]
+
     def _run_round(self, spec: RoundSpec) -> RoundResult:
         if self.mode == "dist":
-            self.transport.broadcast_object(("round", spec), src=0)
-            return self.workers[0].run_round(spec)
+            return self._run_rounds([spec] + [None] * (self.R - 1))[0]
         if self.P == 1:
             return self.workers[0].run_round(spec)
         results: List[Optional[RoundResult]] = [None] * self.P
@@ -147,7 +171,7 @@ class Engine:
         while True:
             cmd = self.transport.broadcast_object(None, src=0)
             if cmd[0] == "round":
-                self.workers[0].run_round(cmd[1])
+                self._dist_round(cmd[1])
             elif cmd[0] == "stop":
                 break
             else:
@@ -192,32 +216,42 @@ class Engine:
                                  f"exceeds the context limit {self.max_seq}")
         outs: List[List[int]] = [[] for _ in prompts]
         todo = [i for i, sp in enumerate(params) if sp.max_new_tokens > 0]
-        cap = self.slots.capacity
+        cap, R = self.slots.capacity, self.R
         with self._lock:
             if not self.healthy:
                 raise RuntimeError(f"engine unhealthy: {self.last_error}")
-            for c0 in range(0, len(todo), cap):
-                idx = todo[c0:c0 + cap]
-                slots = self.slots.alloc(len(idx))
+            for c0 in range(0, len(todo), cap * R):
+                chunk = todo[c0:c0 + cap * R]
+                # contiguous, balanced share per pipeline replica
+                parts = [chunk[round(j * len(chunk) / R): round((j + 1) * len(chunk) / R)]
+                         for j in range(R)]
+                slots = [self.slot_pools[j].alloc(len(part)) if part else []
+                         for j, part in enumerate(parts)]
                 try:
-                    spec = self.make_round([prompts[i] for i in idx], [params[i] for i in idx], slots,
-                                           microbatches, record_timing=record_timing)
+                    specs = [self.make_round([prompts[i] for i in part], [params[i] for i in part],
+                                             slots[j], microbatches, record_timing=record_timing)
+                             if part else None for j, part in enumerate(parts)]
                     t0 = time.perf_counter()
-                    res = self._run_round(spec)
+                    results = self._run_rounds(specs)
                     self.stats["busy_s"] += time.perf_counter() - t0
-                    self.last_round = res
+                    self.last_round = results[0]
                 except Exception as e:
                     self.healthy = False
                     self.last_error = f"{type(e).__name__}: {e}"
                     raise
                 finally:
-                    self.slots.free(slots)
-                toks = torch.cat([t.t() for t in res.tokens], 0)  # [n, steps]
-                for row, i in enumerate(idx):
-                    ids = toks[row, : params[i].max_new_tokens].tolist()
-                    if params[i].stop_at_eos and self.mcfg.eos_token_id in ids:
-                        ids = ids[: ids.index(self.mcfg.eos_token_id) + 1]
-                    outs[i] = ids
+                    for j, sl in enumerate(slots):
+                        if sl:
+                            self.slot_pools[j].free(sl)
+                for part, res in zip(parts, results):
+                    if not part:
+                        continue
+                    toks = torch.cat([t.t() for t in res.tokens], 0)  # [n, steps]
+                    for row, i in enumerate(part):
+                        ids = toks[row, : params[i].max_new_tokens].tolist()
+                        if params[i].stop_at_eos and self.mcfg.eos_token_id in ids:
+                            ids = ids[: ids.index(self.mcfg.eos_token_id) + 1]
+                        outs[i] = ids
                 self.stats["rounds"] += 1
         self.stats["requests"] += len(prompts)
         self.stats["tokens"] += sum(len(o) for o in outs)
@@ -275,6 +309,11 @@ def build_engine(cfg: EngineConfig, **kw) -> Engine:
     """Pick local vs dist from the environment (torchrun sets WORLD_SIZE)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
-        cfg = cfg.replace(num_stages=world)
+        R = max(1, cfg.dp_replicas)
+        if R == 1 and 1 < cfg.num_stages < world and world % cfg.num_stages == 0:
+            R = world // cfg.num_stages  # NUM_STAGES given: the rest is data parallel
+        if world % R:
+            raise ValueError(f"WORLD_SIZE {world} is not a multiple of dp_replicas {R}")
+        cfg = cfg.replace(num_stages=world // R, dp_replicas=R)
         return Engine(cfg, mode="dist", **kw)
     return Engine(cfg, mode="local", **kw)

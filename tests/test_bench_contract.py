@@ -1,0 +1,48 @@
+"""bench.py driver contract, rehearsed on CPU: one JSON line from rank 0 with
+the required fields, N>1 under torch.distributed.run (gloo), incl. PP x DP."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("n,dp", [(1, 1), (2, 1), (4, 2)])
+def test_bench_json_contract(n, dp):
+    args = ["--gpus", str(n), "--dp", str(dp), "--device", "cpu", "--transport", "gloo",
+            "--model", "gpt2-test", "--batch", "2", "--prompt", "4", "--gen", "3",
+            "--steps", "2", "--warmup", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    if n == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    else:
+        port = str(_port())
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only, exactly one line
+    d = json.loads(lines[0])
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert d["config"]["global_batch"] == 2 * n
+    assert d["config"]["parallelism"] == f"pp{n // dp}" + (f"xdp{dp}" if dp > 1 else "")
+    # value is the whole-job token rate over the timed steps
+    toks = d["config"]["global_batch"] * d["config"]["gen_tokens"]
+    assert d["value"] == pytest.approx(toks / (d["ms_per_step"] / 1e3), rel=0.02)

@@ -25,7 +25,9 @@ def _port():
     return p
 
 
-def test_two_rank_pipeline_matches_single_gpu(tmp_path):
+@pytest.mark.parametrize("dp", [1, 2])
+def test_two_rank_pipeline_matches_single_gpu(tmp_path, dp):
+    """dp=1: one 2-stage pipeline; dp=2: two 1-stage replicas sharing the requests."""
     prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 40)), [7] * 9]
     script = tmp_path / "w.py"
     script.write_text(textwrap.dedent(f"""
@@ -34,7 +36,7 @@ def test_two_rank_pipeline_matches_single_gpu(tmp_path):
         from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
         from llm_sharding_demo_amd.runtime.engine import build_engine
         cfg = EngineConfig(model_id="gpt2-test", max_batch=8, device="cuda", transport="gloo",
-                           num_microbatches=2, max_seq_len=128)
+                           num_microbatches=2, max_seq_len=128, dp_replicas={dp})
         eng = build_engine(cfg)
         if eng.rank != 0:
             eng.worker_loop()

@@ -136,9 +136,10 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_multiprocess_pipeline(golden, tmp_path, world):
-    """One process per stage, torch.distributed gloo (the RCCL path's twin)."""
+@pytest.mark.parametrize("world,dp", [(2, 1), (3, 1), (4, 2), (2, 2)])
+def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp):
+    """One process per stage, torch.distributed gloo (the RCCL path's twin);
+    dp > 1: `dp` pipeline replicas of world/dp stages share the requests."""
     script = tmp_path / "w.py"
     script.write_text(textwrap.dedent(f"""
         import sys, json, torch
@@ -146,8 +147,9 @@ def test_gloo_multiprocess_pipeline(golden, tmp_path, world):
         from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
         from llm_sharding_demo_amd.runtime.engine import build_engine
         cfg = EngineConfig(model_id="gpt2-test", max_batch=8, device="cpu", transport="gloo",
-                           num_microbatches=2)
+                           num_microbatches=2, dp_replicas={dp})
         eng = build_engine(cfg)
+        assert (eng.P, eng.R) == ({world // dp}, {dp})
         if eng.rank != 0:
             eng.worker_loop()
         else:
