@@ -111,7 +111,7 @@ void run_gemm(GemmParams& p, int epi, bool tiled, int64_t splits,
   int* cnt = nullptr;
   float* ws = nullptr;
   torch::Tensor wsbuf;
-  if (!tiled) {
+  if (!tiled && epi != EPI_SLAB) {
     const int nw = epi == EPI_SILU_MUL ? 2 : 1;
     TORCH_CHECK(p.N % (64 * nw) == 0, what, ": N must be a multiple of ", 64 * nw);
     const long tiles = p.N / (64 * nw);
@@ -160,24 +160,23 @@ torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, bool tiled, int64_t s
   return out;
 }
 
-// x += a @ w^T + bias.  Decode path: any split, combined in-kernel.  Tiled
-// path with splits > 1: returns fp32 slabs [splits, M, N] that the next norm
-// folds in.
+// x += a @ w^T + bias.  Decode path: any split, combined in-kernel -- or,
+// with defer, like the tiled path with splits > 1: returns the fp32 partial
+// slabs [splits, M, N] (bias not applied) that the next norm folds in.
 c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
                                               c10::optional<torch::Tensor> bias, torch::Tensor x,
                                               int64_t splits, bool tiled,
-                                              c10::optional<torch::Tensor> counters) {
+                                              c10::optional<torch::Tensor> counters, bool defer) {
   GemmParams p = base_params(a, w, tiled);
   need(x, torch::kFloat32, "x");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(0) == p.M && x.size(1) == p.N,
               "residual x must be contiguous [M, N]");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "residual x must be 16-byte aligned");
   if (p.M == 0) return c10::nullopt;
-  if (tiled && splits > 1) {
-    TORCH_CHECK(splits <= p.K / 64, "splits must be <= K/64");
+  if ((tiled || defer) && splits > 1) {
     auto slab = torch::empty({splits, p.M, p.N}, x.options());
     p.slab = slab.data_ptr<float>();
-    run_gemm(p, EPI_SLAB, true, splits, c10::nullopt, x, "linear_residual(split)");
+    run_gemm(p, EPI_SLAB, tiled, splits, c10::nullopt, x, "linear_residual(split)");
     return slab;
   }
   p.bias = opt_bias(bias, p.N);

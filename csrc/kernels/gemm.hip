@@ -209,7 +209,13 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 // 32-k MFMA steps per round: 16 (512 k) up to M = 64; 8 (256 k) for M <= 128
 // so the A image stays at 64 KiB (2 blocks / CU) while the rows double.
 template <int MT>
-constexpr int sk_round_steps() { return MT > 4 ? 8 : 16; }
+constexpr int sk_round_steps() {
+#ifdef LSD_SK_ROUND
+  return LSD_SK_ROUND;
+#else
+  return MT > 4 ? 8 : 16;
+#endif
+}
 
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)g,
@@ -316,7 +322,10 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
   }
   LSD_STAMP(2)
 
-  if (S > 1) {
+  // EPI_SLAB (deferred combine): every split writes its raw partial tile to
+  // slab[split] and the consumer (the next norm kernel, which reads the rows
+  // anyway) sums the S slabs -- no publish, ticket or reducer tail here.
+  if (S > 1 && EPI != EPI_SLAB) {
     // ---- publish this split's partial tile; the last arriver combines.
     // Slab layout is lane-major ([wave][mt][ns][lane] x f32x4) so every lane
     // moves 16 contiguous bytes; stores are write-through (sc1) and every
@@ -390,7 +399,7 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
     } else {
 #pragma unroll
       for (int ns = 0; ns < NW; ++ns)
-        epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns], 0);
+        epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns], split);
     }
   }
   LSD_STAMP(5)
@@ -787,8 +796,7 @@ extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt
     LSD_DISPATCH(EPI_F32)
     LSD_DISPATCH(EPI_RESID)
     LSD_DISPATCH(EPI_QKV)
-    case EPI_SLAB:
-      return tiled ? launch_tiled<EPI_SLAB>(*p, st) : hipErrorInvalidValue;
+    LSD_DISPATCH(EPI_SLAB)
     default: return hipErrorInvalidValue;
   }
 #undef LSD_DISPATCH

@@ -72,7 +72,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     inc, abi, torch_lib = _torch_flags()
     hdrs = headers()
     kflags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-              "-Wno-unused-result"]
+              "-Wno-unused-result"] + os.environ.get("LSD_HIPCC_FLAGS", "").split()  # tuning A/B
     jobs = []
     objs = []
     for k in KERNELS:

@@ -84,6 +84,7 @@ class HipBackend(Backend):
     # decode GEMM: aim for this many workgroups (column tiles x k-splits)
     # decode (split-K, last-arriver) GEMM up to this many rows; tiled above
     SK_MAX_M = int(os.environ.get("LSD_SK_MAX_M", "128"))
+    DEFER_RESID = os.environ.get("LSD_DEFER_RESID", "1") == "1"
     SK_TARGET = int(os.environ.get("LSD_SK_TARGET", "384"))
     SK_MIN_STEPS = int(os.environ.get("LSD_SK_MIN_STEPS", "2"))  # 32-k steps per split
 
@@ -136,6 +137,11 @@ class HipBackend(Backend):
         if self._tiled(M):
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
             return max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
+        if self.DEFER_RESID:
+            # deferred slabs cost S x M x N x 4 B of writes + norm reads, so
+            # fewer, longer splits win (measured, tools/microbench.py resid):
+            # ~800 k per split, 4..8 splits
+            return max(1, min(8, max(4, K // 800), K // 64))
         return self._sk_splits(N, K)
 
     def _sk_splits(self, N: int, K: int, nw: int = 1) -> int:
@@ -209,7 +215,11 @@ class HipBackend(Backend):
         M, K = a.shape
         N = w.shape[0]
         splits = self._resid_splits(M, N, K)
-        slab = self.C.linear_residual(a, w, b, r.x, splits, self._tiled(M), self.counters)
+        tiled = self._tiled(M)
+        # decode split-K: hand the S partial slabs to the next norm (which
+        # reads the rows anyway) instead of a last-arriver reduce in the GEMM
+        defer = self.DEFER_RESID and not tiled and splits > 1
+        slab = self.C.linear_residual(a, w, b, r.x, splits, tiled, self.counters, defer)
         if slab is not None:
             r.pending.append((slab, b))
 

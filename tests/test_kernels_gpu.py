@@ -86,13 +86,15 @@ def test_linear(C, CNT, M, act, splits):
 
 
 @pytest.mark.parametrize("M,splits", [(3, 1), (16, 4), (64, 5), (64, 16), (100, 1), (128, 5), (130, 3)])
-def test_linear_residual_and_f32(C, CNT, M, splits):
+@pytest.mark.parametrize("defer", [False, True])
+def test_linear_residual_and_f32(C, CNT, M, splits, defer):
     N, K = 256, 1024
     a, w, bias = bf(M, K, seed=8), bf(N, K, scale=0.05, seed=9), bf(N, scale=0.1, seed=10)
     tiled = M > 128
     x = torch.randn(M, N, device=DEV)
     x_ref = x + ref.linear(a, w, bias)
-    slab = C.linear_residual(a, w, bias, x, splits, tiled, CNT)
+    slab = C.linear_residual(a, w, bias, x, splits, tiled, CNT, defer)
+    assert (slab is not None) == ((tiled or defer) and splits > 1)
     if slab is not None:
         C.norm(x, slab, bias, None, None, 0.0, True, None, False)
     close(x, x_ref, 2e-3, 1e-3)
@@ -139,12 +141,12 @@ def test_big_gemm_epilogues(BIG, CNT, M, K):
     close(C.linear_f32(a, w, True, 1, CNT), ref.linear(a, w), 2e-3, 1e-3)
     x = torch.randn(M, N, device=DEV)
     x_ref = x + y_ref
-    assert C.linear_residual(a, w, bias, x, 1, True, CNT) is None
+    assert C.linear_residual(a, w, bias, x, 1, True, CNT, False) is None
     close(x, x_ref, 2e-3, 1e-3)
     if K >= 128:
         x = torch.randn(M, N, device=DEV)
         x_ref = x + y_ref
-        slab = C.linear_residual(a, w, bias, x, 2, True, CNT)
+        slab = C.linear_residual(a, w, bias, x, 2, True, CNT, False)
         C.norm(x, slab, bias, None, None, 0.0, True, None, False)
         close(x, x_ref, 2e-3, 1e-3)
 

@@ -74,18 +74,21 @@ def bench_gemm(M, N, K, act=0, resid=False, label=""):
     a = torch.randn(M, K, device=DEV).bfloat16()
     x = torch.randn(M, N, device=DEV)
     it = [0]
-    tiled = M > 64
     be = __import__("llm_sharding_demo_amd.ops.hip", fromlist=["HipBackend"]).HipBackend()
 
     be.counters = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
     nw = 2 if act == 2 else 1
-    tiled_, splits = be._gemm_kw(M, N, K, nw)
+    tiled, splits = be._gemm_kw(M, N, K, nw)
+    if resid:
+        splits = be._resid_splits(M, N, K)
 
     def run():
         w = ws[it[0] % len(ws)]
         it[0] += 1
-        if resid:
-            C.linear_residual(a, w, None, x, be._resid_splits(M, N, K), tiled, be.counters)
+        if resid:  # + the combine the engine pairs it with (deferred slabs -> norm)
+            slab = C.linear_residual(a, w, None, x, splits, tiled, be.counters, be.DEFER_RESID)
+            if slab is not None:
+                C.norm(x, slab, None, None, None, 0.0, True, None, False)
         else:
             C.linear(a, w, None, act, tiled, splits, be.counters)
 
@@ -98,7 +101,8 @@ def bench_gemm(M, N, K, act=0, resid=False, label=""):
         torch.matmul(a, w.t())
 
     ut = timeit(tm)
-    report(f"gemm{label} M={M} N={N} K={K} S={splits}", us, N * K * 2, {"hipblaslt_us": round(ut, 2)})
+    report(f"gemm{label} M={M} N={N} K={K} S={splits}{' tiled' if tiled else ''}", us, N * K * 2,
+           {"hipblaslt_us": round(ut, 2)})
 
 
 def bench_prefill_gemms(T, H, F, nh, hd, label=""):
@@ -122,9 +126,9 @@ def bench_prefill_gemms(T, H, F, nh, hd, label=""):
         ("qkv", lambda: C.linear_qkv(a, wq, bq, kc, vc, slot, pos, H, H, hd, None, True, 1, None),
          lambda: torch.matmul(a, wq.t()), 3 * H, H),
         ("fc_gelu", lambda: C.linear(a, wf, bf, 1, True, 1, None), lambda: torch.matmul(a, wf.t()), F, H),
-        ("proj_resid", lambda: C.linear_residual(a, wp, None, x, 1, True, None),
+        ("proj_resid", lambda: C.linear_residual(a, wp, None, x, 1, True, None, False),
          lambda: torch.matmul(a, wp.t()), H, H),
-        ("proj2_resid", lambda: C.linear_residual(af, wp2, None, x, 1, True, None),
+        ("proj2_resid", lambda: C.linear_residual(af, wp2, None, x, 1, True, None, False),
          lambda: torch.matmul(af, wp2.t()), H, F),
     ]
     for name, fn, ref, N, K in cases:
@@ -139,6 +143,27 @@ def bench_prefill_gemms(T, H, F, nh, hd, label=""):
                {"TFLOP/s": round(fl / us / 1e6, 1), "tile128_us": round(u128, 2),
                 "tile128_TFLOP/s": round(fl / u128 / 1e6, 1), "hipblaslt_us": round(ut, 2),
                 "hipblaslt_TFLOP/s": round(fl / ut / 1e6, 1)})
+
+
+def bench_resid_norm(M, N, K, splits_list, label=""):
+    """Residual GEMM + the following LayerNorm, two ways: split-K combined in
+    the GEMM (last arriver) vs deferred slabs combined by the norm kernel."""
+    ws = rotating(lambda: torch.randn(N, K, device=DEV).bfloat16(), N * K * 2)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    x = torch.randn(M, N, device=DEV)
+    bias = torch.randn(N, device=DEV).bfloat16()
+    g = torch.ones(N, device=DEV).bfloat16()
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    it = [0]
+    for S in splits_list:
+        for defer in (False, True):
+            def run():
+                w = ws[it[0] % len(ws)]
+                it[0] += 1
+                slab = C.linear_residual(a, w, bias, x, S, False, cnt, defer)
+                C.norm(x, slab, bias if slab is not None else None, g, bias, 1e-5, False, None, True)
+            us = timeit(run)
+            report(f"resid+norm{label} M={M} N={N} K={K} S={S} defer={int(defer)}", us, N * K * 2)
 
 
 def bench_attn_decode(B, nh, n_kv, hd, ctx, slots=None):
@@ -237,7 +262,7 @@ def main():
         for tgt in (128, 256, 384, 512, 768, 1024):
             HipBackend.SK_TARGET = tgt
             print("SK_TARGET", tgt, flush=True)
-            for M in (16, 64):
+            for M in (64, 128):
                 bench_gemm(M, 3 * H, H, label="_qkv")
                 bench_gemm(M, F, H, act=1, label="_fc")
                 bench_gemm(M, H, H, resid=True, label="_proj")
@@ -253,6 +278,10 @@ def main():
         for M in (1, 64):
             bench_gemm(M, V, H, act=0, label="_lmhead")
         bench_gemm(8192, 3 * H, H, label="_prefill_qkv")
+    if "resid" in which:
+        for M in (64, 128):
+            bench_resid_norm(M, H, H, (4, 6, 8, 12, 16), label="_proj")
+            bench_resid_norm(M, H, F, (4, 6, 8, 12, 16, 25), label="_proj2")
     if "prefill" in which:
         bench_prefill_gemms(8192, H, F, 25, 64)
         bench_prefill_gemms(4096, 4096, 14336, 32, 128, label="_llama")
