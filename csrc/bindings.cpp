@@ -18,7 +18,11 @@ using lsd::GemmParams;
 extern "C" {
 hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws, hipStream_t st);
 void lsd_gemm_set_big_min(int v);
-int lsd_gemm_sk_rows(int M);
+int lsd_gemm_sk_rows(int M, int N, int S);
+int lsd_gemm_sk_rblocks(int M, int N, int S);
+int lsd_gemm_sk_nw(int M, int epi);
+void lsd_gemm_set_nw2_rows(int v);
+void lsd_gemm_set_sk_rows(int v);
 hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte, const bf16* wpe, float* out,
                      int T, int H, int vocab, hipStream_t st);
 hipError_t lsd_norm(float* x, const float* slab, int splits, const bf16* pbias, const bf16* w,
@@ -112,16 +116,17 @@ void run_gemm(GemmParams& p, int epi, bool tiled, int64_t splits,
   float* ws = nullptr;
   torch::Tensor wsbuf;
   if (!tiled && epi != EPI_SLAB) {
-    const int nw = epi == EPI_SILU_MUL ? 2 : 1;
-    TORCH_CHECK(p.N % (64 * nw) == 0, what, ": N must be a multiple of ", 64 * nw);
-    const long tiles = p.N / (64 * nw);
+    const int nw = lsd_gemm_sk_nw(p.M, epi);  // column tile = 64 * nw (partial last tile masked)
+    if (epi == EPI_SILU_MUL)
+      TORCH_CHECK(p.N % (64 * nw) == 0, what, ": N must be a multiple of ", 64 * nw);
+    const long tiles = (p.N + 64 * nw - 1) / (64 * nw) * lsd_gemm_sk_rblocks(p.M, p.N, (int)splits);
     if (splits > 1) {
       TORCH_CHECK(counters.has_value(), what, ": split-K needs the ticket counter buffer");
       need(*counters, torch::kInt32, "counters");
       TORCH_CHECK(counters->is_contiguous() && counters->numel() >= tiles,
                   what, ": counter buffer too small (", counters->numel(), " < ", tiles, ")");
       cnt = counters->data_ptr<int>();
-      const long rows = lsd_gemm_sk_rows(p.M);  // rows of the launched row tile
+      const long rows = lsd_gemm_sk_rows(p.M, p.N, (int)splits);  // rows per row block
       const long bytes = tiles * splits * rows * 64 * nw * 4;
       TORCH_CHECK(splits * rows * 64 * nw * 4 < (1L << 31), what, ": split workspace too large");
       wsbuf = torch::empty({bytes / 4}, like.options().dtype(torch::kFloat32));
@@ -401,5 +406,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_stamps", &set_stamps);
   // tiled GEMMs with >= this many 256x256 tiles use the pipelined 256^2 kernel
   m.def("gemm_set_big_min", [](int64_t v) { lsd_gemm_set_big_min((int)v); });
+  // decode GEMM: rows per row block (M above it runs as several row blocks)
+  m.def("gemm_set_sk_rows", [](int64_t v) { lsd_gemm_set_sk_rows((int)v); });
+  m.def("gemm_sk_rblocks", [](int64_t M, int64_t N, int64_t S) { return lsd_gemm_sk_rblocks((int)M, (int)N, (int)S); });
+  // decode GEMM column tile 128 (NW = 2) above this many rows
+  m.def("gemm_set_nw2_rows", [](int64_t v) { lsd_gemm_set_nw2_rows((int)v); });
+  m.def("gemm_sk_nw", [](int64_t M, int64_t epi) { return lsd_gemm_sk_nw((int)M, (int)epi); });
   m.attr("arch") = "gfx950";
 }

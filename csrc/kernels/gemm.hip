@@ -226,7 +226,8 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
 // when p.stamps != null; slot 7 = XCC id.  Never on in production.
 #define LSD_STAMP(k)                                                                       \
   if (p.stamps && threadIdx.x == 0)                                                        \
-    p.stamps[((long)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
+    p.stamps[(((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + (k)] = \
+        __builtin_amdgcn_s_memrealtime();
 
 template <int MT, int NW, int EPI>
 __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restrict__ cnt,
@@ -241,18 +242,24 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
 
   LSD_STAMP(0)
   if (p.stamps && threadIdx.x == 0)
-    p.stamps[((long)blockIdx.y * gridDim.x + blockIdx.x) * 8 + 7] =
+    p.stamps[(((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + 7] =
         __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID[3:0]
   const int lane = lane_id(), w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int tile = blockIdx.x, split = blockIdx.y, S = p.splits;
+  const int split = blockIdx.y, S = p.splits;
+  // row block (blockIdx.z): M > rows-per-block runs as independent row
+  // blocks that share each W tile through L2, instead of deeper K splits
+  const int rb0 = blockIdx.z * ROWS;
+  const int tile = blockIdx.x;
+  const int tile_id = blockIdx.z * gridDim.x + tile;  // ticket / workspace index
   const int n_w = tile * BNB + w * 16 * NW;
   const int KT = p.K >> 5;
   const int kb = (int)((long)KT * split / S), ke = (int)((long)KT * (split + 1) / S);
 
   const bf16* wrow[NW];
 #pragma unroll
-  for (int ns = 0; ns < NW; ++ns) wrow[ns] = p.W + (long)(n_w + 16 * ns + r) * p.ldw + g * 8;
+  // a partial last tile (N % (64 NW) != 0) re-reads row N-1; its columns are never stored
+  for (int ns = 0; ns < NW; ++ns) wrow[ns] = p.W + (long)min(n_w + 16 * ns + r, p.N - 1) * p.ldw + g * 8;
 
   f32x4 acc[MT][NW];
 #pragma unroll
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
       const int row = q * 4 + (lane >> 4);
       const int lch = (lane & 15) ^ (row & 15);
       const int kk = min((k0 + c * 4) * 32 + lch * 8, p.K - 8);
-      glds16(p.A + (long)min(row, p.M - 1) * p.lda + kk, smem + c * CHUNK_BYTES + q * 1024);
+      glds16(p.A + (long)min(rb0 + row, p.M - 1) * p.lda + kk, smem + c * CHUNK_BYTES + q * 1024);
     }
     __syncthreads();  // vmcnt(0): the A image and this wave's W fragments have landed
     if (k0 == kb) { LSD_STAMP(1) }
@@ -334,7 +341,7 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
     // block cost ~5 us here).
     constexpr int PER_BLOCK = 4 * MT * NW * 64;  // f32x4 per split tile
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        ws + (long)tile * S * PER_BLOCK * 4, (short)0, S * PER_BLOCK * 16, 0x00020000);
+        ws + (long)tile_id * S * PER_BLOCK * 4, (short)0, S * PER_BLOCK * 16, 0x00020000);
     const int lane_off = ((w * MT * NW) * 64 + lane) * 16;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -346,9 +353,9 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      const int t = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int t = __hip_atomic_fetch_add(cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *s_flag = (t == S - 1);
-      if (t == S - 1) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == S - 1) __hip_atomic_store(cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     LSD_STAMP(3)
@@ -391,15 +398,15 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
 
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int row0 = mt * 16 + 4 * g;
+    const int row0 = rb0 + mt * 16 + 4 * g;
     if constexpr (EPI == EPI_SILU_MUL) {
 #pragma unroll
       for (int ns = 0; ns < NW; ns += 2)
         epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns + 1], 0);
     } else {
 #pragma unroll
-      for (int ns = 0; ns < NW; ++ns)
-        epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns], split);
+      for (int ns = 0; ns < NW; ++ns)  // 16-column sub-tiles past N: wave-uniform skip
+        if (n_w + 16 * ns < p.N) epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns], split);
     }
   }
   LSD_STAMP(5)
@@ -737,19 +744,38 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m
 // Host launchers
 // ---------------------------------------------------------------------------
 static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
-// Row tiles (16 rows each) of the decode kernel launched for M rows: MT is
-// instantiated for {1, 2, 3, 4, 6, 8}.  The split-K workspace is sized from
-// this (lsd_gemm_sk_rows), so the two can never disagree.
-static int sk_mt(int M) {
-  const int mt = (M + 15) / 16;
+// Decode GEMM row blocking: when the column tiles x K splits leave the chip
+// under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
+// with N = H), M > g_sk_rows rows run as ceil(M / g_sk_rows) row blocks
+// (grid z) that share each W tile through L2 -- more workgroups without more
+// split-K slab traffic (tools/microbench.py rows: H x H projection at M = 128
+// 14.1 -> 12.1 us; well-filled grids gain nothing, lm_head loses).
+static int g_sk_rows = 64;
+static int g_rb_fill = 192;
+static int sk_rblocks(int M, int N, int S) {
+  if (M <= g_sk_rows || (N / 64) * S >= g_rb_fill) return 1;
+  return (M + g_sk_rows - 1) / g_sk_rows;
+}
+// Row tiles (16 rows each) of one row block: MT is instantiated for
+// {1, 2, 3, 4, 6, 8}.  The split-K workspace is sized from this
+// (lsd_gemm_sk_rows = row blocks x rows per block), so the two never disagree.
+static int sk_mt(int M, int rb) {
+  const int mt = ((M + rb - 1) / rb + 15) / 16;
   return mt == 5 || mt == 7 ? mt + 1 : mt;
 }
 
-template <int EPI>
-static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
-  constexpr int NW = (EPI == EPI_SILU_MUL) ? 2 : 1;
-  const int MT = sk_mt(p.M);
-  dim3 grid(p.N / (64 * NW), p.splits), block(256);
+// Column tile width: 64 * NW.  Wide tiles (NW = 2) read A half as often but
+// double the weight fragments per wave; measured slower at M = 128 on every
+// GPT-2 XL shape (tools/microbench.py rows), so only silu_mul (gate/up pairs)
+// uses them by default; lsd_gemm_set_nw2_rows() lowers the row threshold.
+static int g_nw2_rows = 1 << 30;
+static int sk_nw(int M, int epi) { return (epi == EPI_SILU_MUL || M > g_nw2_rows) ? 2 : 1; }
+
+template <int EPI, int NW>
+static hipError_t launch_sk_nw(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
+  const int RB = sk_rblocks(p.M, p.N, p.splits);
+  const int MT = sk_mt(p.M, RB);
+  dim3 grid((p.N + 64 * NW - 1) / (64 * NW), p.splits, RB), block(256);
   switch (MT) {
     case 1: hipLaunchKernelGGL((gemm_sk_kernel<1, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
     case 2: hipLaunchKernelGGL((gemm_sk_kernel<2, NW, EPI>), grid, block, 0, st, p, cnt, ws); break;
@@ -760,6 +786,15 @@ static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+template <int EPI>
+static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
+  if constexpr (EPI == EPI_SILU_MUL) {
+    return launch_sk_nw<EPI, 2>(p, cnt, ws, st);
+  } else {
+    return sk_nw(p.M, EPI) == 2 ? launch_sk_nw<EPI, 2>(p, cnt, ws, st) : launch_sk_nw<EPI, 1>(p, cnt, ws, st);
+  }
 }
 
 template <int EPI>
@@ -782,7 +817,13 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
 using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
-extern "C" int lsd_gemm_sk_rows(int M) { return sk_mt(M) * 16; }
+extern "C" int lsd_gemm_sk_rblocks(int M, int N, int S) { return sk_rblocks(M, N, S); }
+extern "C" int lsd_gemm_sk_rows(int M, int N, int S) {  // rows per row block
+  return sk_mt(M, sk_rblocks(M, N, S)) * 16;
+}
+extern "C" int lsd_gemm_sk_nw(int M, int epi) { return sk_nw(M, epi); }
+extern "C" void lsd_gemm_set_nw2_rows(int v) { g_nw2_rows = v; }
+extern "C" void lsd_gemm_set_sk_rows(int v) { g_sk_rows = v < 16 ? 16 : (v > 128 ? 128 : v); }
 
 // C ABI used by csrc/bindings.cpp; shapes are validated there.
 extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws,

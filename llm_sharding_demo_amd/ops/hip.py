@@ -87,9 +87,16 @@ class HipBackend(Backend):
     DEFER_RESID = os.environ.get("LSD_DEFER_RESID", "1") == "1"
     SK_TARGET = int(os.environ.get("LSD_SK_TARGET", "384"))
     SK_MIN_STEPS = int(os.environ.get("LSD_SK_MIN_STEPS", "2"))  # 32-k steps per split
+    # decode GEMM rows per row block when an under-filled grid (deferred
+    # residual projections) is split into row blocks (sk_rblocks in gemm.hip)
+    SK_ROWS = int(os.environ.get("LSD_SK_ROWS", "64"))
+    # decode GEMM 128-column tiles above this many rows (off: slower, see gemm.hip)
+    NW2_ROWS = int(os.environ.get("LSD_NW2_ROWS", str(1 << 30)))
 
     def __init__(self):
         self.C = _load()
+        self.C.gemm_set_sk_rows(self.SK_ROWS)
+        self.C.gemm_set_nw2_rows(self.NW2_ROWS)
         self.counters = None
         self._rope = None
         self.lane = 0  # microbatch lane (stream) currently being issued; see pipeline.py
@@ -142,16 +149,17 @@ class HipBackend(Backend):
             # fewer, longer splits win (measured, tools/microbench.py resid):
             # ~800 k per split, 4..8 splits
             return max(1, min(8, max(4, K // 800), K // 64))
-        return self._sk_splits(N, K)
+        return self._sk_splits(M, N, K)
 
-    def _sk_splits(self, N: int, K: int, nw: int = 1) -> int:
-        tiles = N // (64 * nw)
+    def _sk_splits(self, M: int, N: int, K: int, nw: int = 1) -> int:
+        nw = max(nw, 2 if M > self.NW2_ROWS else 1)  # mirrors sk_nw() in gemm.hip
+        tiles = math.ceil(N / (64 * nw))  # >= SK_TARGET workgroups: never row-blocked
         return max(1, min(math.ceil(self.SK_TARGET / tiles), K // 32 // self.SK_MIN_STEPS or 1))
 
     def _gemm_kw(self, M: int, N: int, K: int, nw: int = 1):
         if self._tiled(M):
             return True, 1
-        return False, self._sk_splits(N, K, nw)
+        return False, self._sk_splits(M, N, K, nw)
 
     # ------------------------------------------------------------------
     def embed(self, ids, pos, wte, wpe):

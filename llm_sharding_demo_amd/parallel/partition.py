@@ -101,3 +101,140 @@ def make_plan(cfg: ModelConfig, num_stages: int, split_points: Optional[Sequence
     if num_stages == 1:
         return [(0, cfg.n_layers)]
     return auto_partition(cfg, num_stages, batch, avg_ctx)
+
+
+# ---------------------------------------------------------------------------
+# Half-layer ("unit") partitioning
+# ---------------------------------------------------------------------------
+# A transformer block is two residual sub-blocks: unit 2i = attention half of
+# layer i (norm, QKV + KV append, attention, output projection + residual),
+# unit 2i+1 = MLP half (norm, up projection + activation, down projection +
+# residual).  Between the two the residual stream x is the ONLY live state,
+# exactly like between layers, so a stage boundary may sit after either half.
+# With whole layers the last stage's lm_head + sampler can only be balanced in
+# steps of one block: GPT-2 XL on 8 stages has 48 blocks + ~1.2 blocks of head,
+# and any whole-layer split leaves a 7-block stage (86 % of ideal); half-layer
+# cuts get within a few %.
+#
+# The cost model is decode time per microbatch per step (us) on MI355X,
+# calibrated against the kernel profile of the bench config
+# (profiles/r1_xl_b128_2lanes_kernel_stats.csv, 128-row microbatches):
+#   decode GEMM  ~ 4 us + weight bytes / ~1 TB/s (N < 16k), ~2.3 TB/s (lm_head)
+#   attention    ~ 3 us + KV bytes / 5.5 TB/s
+#   norm 6 us, sampler 8 us + 0.37 us/row, embed 4 us.
+UnitPlan = List[Tuple[int, int]]
+
+
+def _gemm_us(n: int, k: int, rows: int) -> float:
+    bw = 2.3e6 if n >= 16384 else 1.0e6  # bytes per us
+    return 4.0 + n * k * 2 / bw + 2.0 * rows * n * k / 1.0e9
+
+
+def unit_costs(cfg: ModelConfig, rows: int = 128, avg_ctx: int = 192) -> Tuple[List[float], float, float]:
+    """(per-unit decode cost [2L], last-stage head cost, first-stage embed cost) in us."""
+    h = cfg.hidden
+    norm = 6.0
+    attn = 3.0 + rows * avg_ctx * cfg.kv_bytes_per_token_per_layer() / 5.5e6
+    if cfg.arch == "gpt2":
+        up = _gemm_us(cfg.ffn, h, rows)
+    else:
+        up = _gemm_us(2 * cfg.ffn, h, rows)
+    a = norm + _gemm_us(cfg.qkv_size, h, rows) + attn + _gemm_us(h, cfg.q_size, rows)
+    m = norm + up + _gemm_us(h, cfg.ffn, rows)
+    head = norm + _gemm_us(cfg.vocab_padded, h, rows) + 8.0 + 0.37 * rows
+    embed = 4.0
+    return [a, m] * cfg.n_layers, head, embed
+
+
+def _minmax_dp(costs: Sequence[float], P: int, head: float) -> UnitPlan:
+    """Exact min-max contiguous partition of `costs` into P non-empty parts;
+    the last part also pays `head` (Python twin of the native runtime's
+    partition_minmax)."""
+    n = len(costs)
+    if not 1 <= P <= n:
+        raise ValueError(f"cannot split {n} units into {P} non-empty stages")
+    pre = [0.0]
+    for c in costs:
+        pre.append(pre[-1] + c)
+    INF = float("inf")
+    best = [[INF] * (n + 1) for _ in range(P + 1)]
+    arg = [[0] * (n + 1) for _ in range(P + 1)]
+    best[0][0] = 0.0
+    for p in range(1, P + 1):
+        for i in range(p, n - (P - p) + 1):
+            for j in range(p - 1, i):
+                c = pre[i] - pre[j] + (head if p == P else 0.0)
+                v = max(best[p - 1][j], c)
+                if v < best[p][i]:
+                    best[p][i], arg[p][i] = v, j
+    plan: UnitPlan = []
+    i = n
+    for p in range(P, 0, -1):
+        j = arg[p][i]
+        plan.append((j, i))
+        i = j
+    plan.reverse()
+    return plan
+
+
+def validate_unit_plan(plan: UnitPlan, n_layers: int) -> None:
+    validate_plan(plan, 2 * n_layers)
+    if any(b <= a for a, b in plan):
+        raise ValueError(f"unit plan {plan} has an empty stage")
+
+
+def unit_stage_costs(cfg: ModelConfig, plan: UnitPlan, rows: int = 128, avg_ctx: int = 192) -> List[float]:
+    costs, head, embed = unit_costs(cfg, rows, avg_ctx)
+    out = []
+    for s, (a, b) in enumerate(plan):
+        c = sum(costs[a:b]) + (embed if s == 0 else 0.0) + (head if s == len(plan) - 1 else 0.0)
+        out.append(c)
+    return out
+
+
+def make_unit_plan(cfg: ModelConfig, num_stages: int, split_points: Optional[Sequence[int]] = None,
+                   split_units: Optional[Sequence[int]] = None, rows: int = 128,
+                   avg_ctx: int = 192, half_layers: bool = True) -> UnitPlan:
+    """Stage ranges in half-layer units.  Explicit `split_units` (unit
+    boundaries) or `split_points` (layer boundaries, SPLIT_AT) win; otherwise
+    the min-max DP over the unit cost model, at half-layer granularity unless
+    `half_layers` is False (then whole layers only)."""
+    L, P = cfg.n_layers, num_stages
+    if split_units:
+        pts = [0] + list(split_units) + [2 * L]
+        plan = [(pts[i], pts[i + 1]) for i in range(len(pts) - 1)]
+    elif split_points:
+        plan = [(2 * a, 2 * b) for a, b in make_plan(cfg, P, split_points)]
+    elif P == 1:
+        plan = [(0, 2 * L)]
+    else:
+        costs, head, embed = unit_costs(cfg, max(1, min(rows, 128)), avg_ctx)
+        if half_layers:
+            plan = _native_or_python_dp(costs, P, head, embed)
+        else:
+            layer = [costs[2 * i] + costs[2 * i + 1] for i in range(L)]
+            plan = [(2 * a, 2 * b) for a, b in _native_or_python_dp(layer, P, head, embed)]
+    if len(plan) != P:
+        raise ValueError(f"unit plan {plan} has {len(plan)} stages, but num_stages={P}")
+    validate_unit_plan(plan, L)
+    return plan
+
+
+def _native_or_python_dp(costs, P, head, first) -> UnitPlan:
+    import os
+
+    from ..runtime import native
+
+    costs = list(costs)
+    costs[0] += first  # stage 0 always owns unit 0
+    if not 1 <= P <= len(costs):
+        raise ValueError(f"cannot split {len(costs)} units into {P} non-empty stages")
+    mod = native.load()
+    if mod is not None and os.environ.get("LSD_PY_RUNTIME", "0") != "1":
+        return [tuple(x) for x in mod.partition_minmax(costs, P, head)]
+    return _minmax_dp(costs, P, head)
+
+
+def units_to_layers(plan: UnitPlan) -> Plan:
+    """Layers each stage touches (a layer cut in half appears in both stages)."""
+    return [(a // 2, (b + 1) // 2) for a, b in plan]

@@ -269,6 +269,19 @@ def main():
                 bench_gemm(M, H, F, resid=True, label="_proj2")
                 bench_gemm(M, V, H, label="_lmhead")
         HipBackend.SK_TARGET = 384
+    if "rows" in which:  # decode GEMM: row blocks x column tile x split target at M = 128
+        from llm_sharding_demo_amd.ops.hip import HipBackend
+        for nw2 in (128, 64):
+            for rows in (128, 64):
+                for tgt in (256, 384, 512):
+                    HipBackend.SK_ROWS, HipBackend.SK_TARGET, HipBackend.NW2_ROWS = rows, tgt, nw2
+                    tag = f"_nw{1 if nw2 >= 128 else 2}_r{rows}_t{tgt}"
+                    bench_gemm(128, 3 * H, H, label="_qkv" + tag)
+                    bench_gemm(128, F, H, act=1, label="_fc" + tag)
+                    bench_gemm(128, H, H, resid=True, label="_proj" + tag)
+                    bench_gemm(128, H, F, resid=True, label="_proj2" + tag)
+                    bench_gemm(128, V, H, label="_lmhead" + tag)
+        HipBackend.SK_ROWS, HipBackend.SK_TARGET, HipBackend.NW2_ROWS = 64, 384, 64
     if "gemm" in which:
         for M in (1, 16, 32, 64, 128, 256):
             bench_gemm(M, 3 * H, H, label="_qkv")
@@ -286,7 +299,7 @@ def main():
         bench_prefill_gemms(8192, H, F, 25, 64)
         bench_prefill_gemms(4096, 4096, 14336, 32, 128, label="_llama")
     if "attn" in which:
-        for B in (1, 16, 64):
+        for B in (1, 16, 64, 128):
             bench_attn_decode(B, 25, 25, 64, 192)
         bench_attn_decode(64, 25, 25, 64, 1024)
         bench_attn_decode(64, 32, 8, 128, 512)
@@ -294,8 +307,9 @@ def main():
         bench_attn_prefill(4, 1024, 25, 25, 64)
         bench_attn_prefill(4, 1024, 32, 8, 128)
     if "norm" in which:
-        for s in (0, 4, 6):
+        for s in (0, 4, 8):
             bench_norm(64, H, s)
+            bench_norm(128, H, s)
     if "sample" in which:
         for g in (True, False):
             bench_sample(64, 50257, g)
