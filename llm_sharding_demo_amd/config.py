@@ -212,6 +212,13 @@ class EngineConfig:
     dp_replicas: int = 1
     # Explicit split points (len num_stages-1), e.g. SPLIT_AT=2 -> [2].  None = cost model.
     split_points: Optional[Sequence[int]] = None
+    # Explicit split points in half-layer units: a stage starts at unit u, where
+    # u = 2i is layer i's attention half and u = 2i + 1 its MLP half, e.g.
+    # [13] cuts layer 6 between attention and MLP.
+    split_units: Optional[Sequence[int]] = None
+    # Auto partition may cut between a layer's attention and MLP halves
+    # (finer balance of the last stage's lm_head + sampler).
+    half_layer_split: bool = True
     dtype: str = "bf16"  # compute / storage dtype on GPU; CPU golden runs in fp32
     device: str = "auto"  # "auto" -> cuda if available else cpu
     max_batch: int = 64  # max concurrent sequences (KV slots)

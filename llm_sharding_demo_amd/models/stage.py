@@ -9,11 +9,15 @@ to P stages with an arbitrary layer range each.  Differences by design:
   * K/V are appended to the shard-local cache, so decode processes one token
     per sequence (quirk Q5),
   * the last stage computes lm_head for the last position of each sequence
-    only (quirk Q6) unless `all_logits` is requested (compat /forward_b).
+    only (quirk Q6) unless `all_logits` is requested (compat /forward_b),
+  * a stage boundary may fall between the attention and the MLP half of a
+    layer (`units`, parallel/partition.py): unit 2i = attention half of layer
+    i, unit 2i+1 = its MLP half.  Only the residual stream crosses either kind
+    of boundary; the KV cache of layer i lives with its attention half.
 """
 from __future__ import annotations
 
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -21,56 +25,85 @@ from ..config import ModelConfig
 from ..ops import Residual, get_backend
 from ..runtime.batch import BatchMeta
 from ..runtime.kv_cache import KVCache
-from .weights import maybe_load
+from .weights import layer_half, maybe_load
 
 
 class StageModel:
     def __init__(self, cfg: ModelConfig, layer_start: int, layer_end: int, first: bool,
                  last: bool, device="cpu", dtype: Optional[torch.dtype] = None, seed: int = 0,
                  weights_path: Optional[str] = None, max_slots: int = 8, max_seq: int = 1024,
-                 weights: Optional[Dict[str, torch.Tensor]] = None):
+                 weights: Optional[Dict[str, torch.Tensor]] = None,
+                 units: Optional[Tuple[int, int]] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         if dtype is None:
             dtype = torch.float32 if self.device.type == "cpu" else torch.bfloat16
         self.dtype = dtype
-        self.layer_start, self.layer_end = layer_start, layer_end
+        if units is None:
+            units = (2 * layer_start, 2 * layer_end)
+        ua, ub = units
+        if not 0 <= ua <= ub <= 2 * cfg.n_layers:
+            raise ValueError(f"unit range {units} outside [0, {2 * cfg.n_layers}]")
+        self.unit_start, self.unit_end = ua, ub
+        self.layer_start, self.layer_end = ua // 2, (ub + 1) // 2  # layers touched
         self.first, self.last = first, last
-        self.layers = range(layer_start, layer_end)
+        self.layers = range(self.layer_start, self.layer_end)
+        # layers whose attention half (and so whose KV cache) lives here
+        self.kv_layers = [i for i in self.layers if ua <= 2 * i < ub]
+        self._kv_index = {i: j for j, i in enumerate(self.kv_layers)}
         if weights is None:
-            weights = maybe_load(cfg, weights_path, self.layers, first, last, seed, self.device, dtype)
+            weights = maybe_load(cfg, weights_path, self.layers, first, last, seed, self.device, dtype,
+                                 units=units)
         else:
-            weights = {k: v.to(device=self.device, dtype=dtype).contiguous() for k, v in weights.items()}
+            weights = {k: v.to(device=self.device, dtype=dtype).contiguous() for k, v in weights.items()
+                       if self._owns(k)}
         self.w = weights
         self.max_seq = min(max_seq, cfg.max_positions)
-        self.kv = KVCache(len(self.layers), max_slots, cfg.n_kv_heads, self.max_seq,
+        self.kv = KVCache(len(self.kv_layers), max_slots, cfg.n_kv_heads, self.max_seq,
                           cfg.head_dim, dtype, self.device)
         self.backend = get_backend(self.device)
         self.backend.prepare_stage(self)
+
+    def _owns(self, name: str) -> bool:
+        """Is tensor `name` used by this stage (its units, embeddings, head)?"""
+        lh = layer_half(name)
+        if lh is None:
+            emb = name in ("wte", "wpe", "embed_tokens")
+            head = name in ("ln_f.weight", "ln_f.bias", "norm.weight", "lm_head") or (
+                name == "wte" and self.cfg.tie_embeddings)
+            return (emb and self.first) or (head and self.last)
+        return self.unit_start <= 2 * lh[0] + lh[1] < self.unit_end
 
     # ------------------------------------------------------------------
     def _lw(self, i: int, name: str) -> torch.Tensor:
         p = "h." if self.cfg.arch == "gpt2" else "layers."
         return self.w[f"{p}{i}.{name}"]
 
-    def _gpt2_layer(self, li: int, i: int, r: Residual, meta: BatchMeta) -> None:
+    # [tf5.15] modeling_gpt2.py:262-309 GPT2Block.forward, split at the residual
+    def _gpt2_attn(self, li: int, i: int, r: Residual, meta: BatchMeta) -> None:
         be, c, w = self.backend, self.cfg, self._lw
         xn = be.layernorm(r, w(i, "ln_1.weight"), w(i, "ln_1.bias"), c.norm_eps)
         q = be.qkv_kv_append(xn, w(i, "attn.c_attn.weight"), w(i, "attn.c_attn.bias"),
                              self.kv.k(li), self.kv.v(li), meta, c)
         o = be.attention(q, self.kv.k(li), self.kv.v(li), meta)
         be.linear_residual(o, w(i, "attn.c_proj.weight"), w(i, "attn.c_proj.bias"), r)
+
+    def _gpt2_mlp(self, i: int, r: Residual) -> None:
+        be, c, w = self.backend, self.cfg, self._lw
         xn = be.layernorm(r, w(i, "ln_2.weight"), w(i, "ln_2.bias"), c.norm_eps)
         h = be.linear(xn, w(i, "mlp.c_fc.weight"), w(i, "mlp.c_fc.bias"), act="gelu")
         be.linear_residual(h, w(i, "mlp.c_proj.weight"), w(i, "mlp.c_proj.bias"), r)
 
-    def _llama_layer(self, li: int, i: int, r: Residual, meta: BatchMeta) -> None:
+    def _llama_attn(self, li: int, i: int, r: Residual, meta: BatchMeta) -> None:
         be, c, w = self.backend, self.cfg, self._lw
         xn = be.rmsnorm(r, w(i, "input_layernorm.weight"), c.norm_eps)
         q = be.qkv_kv_append(xn, w(i, "self_attn.qkv.weight"), None,
                              self.kv.k(li), self.kv.v(li), meta, c)
         o = be.attention(q, self.kv.k(li), self.kv.v(li), meta)
         be.linear_residual(o, w(i, "self_attn.o_proj.weight"), None, r)
+
+    def _llama_mlp(self, i: int, r: Residual) -> None:
+        be, c, w = self.backend, self.cfg, self._lw
         xn = be.rmsnorm(r, w(i, "post_attention_layernorm.weight"), c.norm_eps)
         h = be.linear(xn, w(i, "mlp.gate_up.weight"), None, act="silu_mul")
         be.linear_residual(h, w(i, "mlp.down_proj.weight"), None, r)
@@ -89,9 +122,15 @@ class StageModel:
         [T, vocab_padded] with all_logits)."""
         x = self.embed(inp, meta) if self.first else inp
         r = Residual(x)
-        layer_fn = self._gpt2_layer if self.cfg.arch == "gpt2" else self._llama_layer
-        for li, i in enumerate(self.layers):
-            layer_fn(li, i, r, meta)
+        gpt2 = self.cfg.arch == "gpt2"
+        attn_fn = self._gpt2_attn if gpt2 else self._llama_attn
+        mlp_fn = self._gpt2_mlp if gpt2 else self._llama_mlp
+        for u in range(self.unit_start, self.unit_end):
+            i = u >> 1
+            if u & 1:
+                mlp_fn(i, r)
+            else:
+                attn_fn(self._kv_index[i], i, r, meta)
         x = self.backend.flush(r)
         if not self.last:
             return x

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import os
 import zlib
-from typing import Dict, Iterable, Optional
+from typing import Dict, Iterable, Optional, Tuple
 
 import torch
 
@@ -73,7 +73,44 @@ def _llama_shapes(cfg: ModelConfig, i: int) -> Dict[str, tuple]:
     }
 
 
-def stage_tensor_shapes(cfg: ModelConfig, layers: Iterable[int], first: bool, last: bool):
+_ATTN_PARTS = ("ln_1.", "attn.", "input_layernorm.", "self_attn.")
+_MLP_PARTS = ("ln_2.", "mlp.", "post_attention_layernorm.")
+
+
+def layer_half(name: str) -> Optional[Tuple[int, int]]:
+    """(layer, 0 = attention half | 1 = MLP half) of a per-layer tensor name,
+    None for embeddings / final norm / lm_head (parallel/partition.py units)."""
+    for pre in ("h.", "layers."):
+        if name.startswith(pre):
+            idx, rest = name[len(pre):].split(".", 1)
+            if rest.startswith(_ATTN_PARTS):
+                return int(idx), 0
+            if rest.startswith(_MLP_PARTS):
+                return int(idx), 1
+            raise ValueError(f"unknown per-layer tensor {name!r}")
+    return None
+
+
+def _filter_units(shapes: Dict[str, tuple], units: Optional[Tuple[int, int]]) -> Dict[str, tuple]:
+    if units is None:
+        return shapes
+    ua, ub = units
+    out = {}
+    for n, s in shapes.items():
+        lh = layer_half(n)
+        if lh is None or ua <= 2 * lh[0] + lh[1] < ub:
+            out[n] = s
+    return out
+
+
+def stage_tensor_shapes(cfg: ModelConfig, layers: Iterable[int], first: bool, last: bool,
+                        units: Optional[Tuple[int, int]] = None):
+    """Tensors a stage materialises; with `units` only the halves of the
+    boundary layers that the stage runs."""
+    return _filter_units(_stage_tensor_shapes(cfg, layers, first, last), units)
+
+
+def _stage_tensor_shapes(cfg: ModelConfig, layers: Iterable[int], first: bool, last: bool):
     shapes: Dict[str, tuple] = {}
     if cfg.arch == "gpt2":
         if first:
@@ -115,8 +152,8 @@ def _init_one(cfg: ModelConfig, name: str, shape, seed: int, device, dtype) -> t
 
 
 def init_stage_weights(cfg: ModelConfig, layers, first: bool, last: bool, seed: int,
-                       device, dtype) -> Dict[str, torch.Tensor]:
-    shapes = stage_tensor_shapes(cfg, layers, first, last)
+                       device, dtype, units=None) -> Dict[str, torch.Tensor]:
+    shapes = stage_tensor_shapes(cfg, layers, first, last, units)
     return {n: _init_one(cfg, n, s, seed, device, dtype) for n, s in shapes.items()}
 
 
@@ -158,10 +195,10 @@ def _open_checkpoint(path: str):
 
 
 def load_stage_weights(cfg: ModelConfig, path: str, layers, first: bool, last: bool,
-                       device, dtype) -> Dict[str, torch.Tensor]:
+                       device, dtype, units=None) -> Dict[str, torch.Tensor]:
     get, keys = _open_checkpoint(path)
     out: Dict[str, torch.Tensor] = {}
-    want = stage_tensor_shapes(cfg, layers, first, last)
+    want = stage_tensor_shapes(cfg, layers, first, last, units)
 
     def find(name):
         for pre in ("", "transformer.", "model."):
@@ -243,7 +280,8 @@ def canonical_to_hf_llama(cfg: ModelConfig, w: Dict[str, torch.Tensor]) -> Dict[
     return {k: v.contiguous() for k, v in sd.items()}
 
 
-def maybe_load(cfg: ModelConfig, weights: Optional[str], layers, first, last, seed, device, dtype):
+def maybe_load(cfg: ModelConfig, weights: Optional[str], layers, first, last, seed, device, dtype,
+               units=None):
     if weights:
-        return load_stage_weights(cfg, weights, layers, first, last, device, dtype)
-    return init_stage_weights(cfg, layers, first, last, seed, device, dtype)
+        return load_stage_weights(cfg, weights, layers, first, last, device, dtype, units)
+    return init_stage_weights(cfg, layers, first, last, seed, device, dtype, units)

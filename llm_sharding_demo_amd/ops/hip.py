@@ -114,10 +114,12 @@ class HipBackend(Backend):
             perm_k = rope_pair_permutation(cfg.n_kv_heads, cfg.head_dim) + cfg.q_size
             keep = torch.arange(cfg.q_size + cfg.kv_size, cfg.qkv_size)
             perm = torch.cat([perm_q, perm_k, keep]).to(dev)
-            for i in stage.layers:
+            for i in stage.layers:  # a boundary layer may hold only one half here
                 p = f"layers.{i}."
-                w[p + "self_attn.qkv.weight"] = w[p + "self_attn.qkv.weight"].index_select(0, perm).contiguous()
-                w[p + "mlp.gate_up.weight"] = interleave_gate_up(w[p + "mlp.gate_up.weight"], cfg.ffn).contiguous()
+                if p + "self_attn.qkv.weight" in w:
+                    w[p + "self_attn.qkv.weight"] = w[p + "self_attn.qkv.weight"].index_select(0, perm).contiguous()
+                if p + "mlp.gate_up.weight" in w:
+                    w[p + "mlp.gate_up.weight"] = interleave_gate_up(w[p + "mlp.gate_up.weight"], cfg.ffn).contiguous()
             stage._rope = rope_table(stage.max_seq, cfg.head_dim, cfg.rope_theta, dev)
         else:
             stage._rope = None

@@ -7,8 +7,10 @@ and shard B uses 1 (`k8s/shard-a-deployment.yaml:22-23`,
 the plan has a single owner (the engine) and is validated to cover every
 layer exactly once.
 
-Auto partitioning minimises the slowest stage under a decode cost model in
-bytes streamed from HBM per step (decode is bandwidth-bound on MI355X):
+The engine partitions at half-layer granularity (`make_unit_plan`, below):
+min-max DP over a per-unit decode time model calibrated on MI355X.  The
+whole-layer API (`make_plan` / `auto_partition`, a bytes model) is kept for
+explicit SPLIT_AT plans and the compat shard roles:
   block i : weight bytes + KV bytes (batch * avg ctx * per-layer KV)
   + a fixed per-block launch overhead expressed in bytes (~1.3 us/kernel
     boundary * 7 kernels at ~5 TB/s)
@@ -117,29 +119,31 @@ def make_plan(cfg: ModelConfig, num_stages: int, split_points: Optional[Sequence
 # cuts get within a few %.
 #
 # The cost model is decode time per microbatch per step (us) on MI355X,
-# calibrated against the kernel profile of the bench config
-# (profiles/r1_xl_b128_2lanes_kernel_stats.csv, 128-row microbatches):
-#   decode GEMM  ~ 4 us + weight bytes / ~1 TB/s (N < 16k), ~2.3 TB/s (lm_head)
-#   attention    ~ 3 us + KV bytes / 5.5 TB/s
+# calibrated against the kernel profile and microbenchmarks of the bench
+# config (profiles/r1_xl_*_kernel_stats.csv, r1_microbench_*; 128-row
+# microbatches, GPT-2 XL: attention half ~70 us, MLP half ~47 us, head ~146 us):
+#   decode GEMM  ~ 5 us + weight bytes / 1.3 TB/s (N < 16k; 2.3 TB/s for
+#                lm_head) + FLOPs / 2 PF; QKV + 6 us (KV-cache scatter, RoPE)
+#   attention    ~ 3 us + KV bytes / 6 TB/s
 #   norm 6 us, sampler 8 us + 0.37 us/row, embed 4 us.
 UnitPlan = List[Tuple[int, int]]
 
 
 def _gemm_us(n: int, k: int, rows: int) -> float:
-    bw = 2.3e6 if n >= 16384 else 1.0e6  # bytes per us
-    return 4.0 + n * k * 2 / bw + 2.0 * rows * n * k / 1.0e9
+    bw = 2.3e6 if n >= 16384 else 1.3e6  # bytes per us
+    return 5.0 + n * k * 2 / bw + 2.0 * rows * n * k / 2.0e9
 
 
 def unit_costs(cfg: ModelConfig, rows: int = 128, avg_ctx: int = 192) -> Tuple[List[float], float, float]:
     """(per-unit decode cost [2L], last-stage head cost, first-stage embed cost) in us."""
     h = cfg.hidden
     norm = 6.0
-    attn = 3.0 + rows * avg_ctx * cfg.kv_bytes_per_token_per_layer() / 5.5e6
+    attn = 3.0 + rows * avg_ctx * cfg.kv_bytes_per_token_per_layer() / 6.0e6
     if cfg.arch == "gpt2":
         up = _gemm_us(cfg.ffn, h, rows)
     else:
         up = _gemm_us(2 * cfg.ffn, h, rows)
-    a = norm + _gemm_us(cfg.qkv_size, h, rows) + attn + _gemm_us(h, cfg.q_size, rows)
+    a = norm + _gemm_us(cfg.qkv_size, h, rows) + 6.0 + attn + _gemm_us(h, cfg.q_size, rows)
     m = norm + up + _gemm_us(h, cfg.ffn, rows)
     head = norm + _gemm_us(cfg.vocab_padded, h, rows) + 8.0 + 0.37 * rows
     embed = 4.0

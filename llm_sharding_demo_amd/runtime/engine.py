@@ -31,7 +31,7 @@ import torch
 from ..config import EngineConfig, SamplingParams
 from ..models.stage import StageModel
 from ..parallel.comm import LocalFabric, Transport, init_distributed, make_dist_transport
-from ..parallel.partition import make_plan
+from ..parallel.partition import make_unit_plan, units_to_layers
 from ..parallel.pipeline import MicroBatchSpec, RoundResult, RoundSpec, StageWorker
 from .kv_cache import SlotAllocator
 
@@ -67,8 +67,13 @@ class Engine:
         if mode == "local" and self.R != 1:
             raise ValueError("dp_replicas > 1 needs the dist mode (one process per GPU)")
         self.replica, self.stage_idx = 0, 0
-        self.plan = make_plan(self.mcfg, self.P, cfg.split_points, batch=cfg.max_batch,
-                              avg_ctx=min(256, cfg.max_seq_len))
+        # stage ranges in half-layer units (parallel/partition.py); `plan` is
+        # the layer view (a layer cut in half is listed in both stages)
+        mb_rows = -(-cfg.max_batch // max(1, cfg.microbatches))
+        self.unit_plan = make_unit_plan(self.mcfg, self.P, cfg.split_points, cfg.split_units,
+                                        rows=mb_rows, avg_ctx=min(192, cfg.max_seq_len),
+                                        half_layers=cfg.half_layer_split)
+        self.plan = units_to_layers(self.unit_plan)
         self._rng = random.Random(cfg.seed)
         self.healthy = True
         self.last_error: Optional[str] = None
@@ -117,7 +122,7 @@ class Engine:
         return StageModel(self.mcfg, a, b, first=(i == 0), last=(i == self.P - 1), device=device,
                           dtype=_dtype(self.cfg.dtype, device), seed=self.cfg.seed,
                           weights_path=self.cfg.weights, max_slots=self.cfg.max_batch,
-                          max_seq=self.max_seq)
+                          max_seq=self.max_seq, units=self.unit_plan[i])
 
     @property
     def is_coordinator(self) -> bool:
@@ -173,6 +178,7 @@ class Engine:
             if cmd[0] == "round":
                 self._dist_round(cmd[1])
             elif cmd[0] == "stop":
+                self._close_dist()
                 break
             else:
                 raise RuntimeError(f"unknown command {cmd[0]!r}")
@@ -180,6 +186,17 @@ class Engine:
     def shutdown(self) -> None:
         if self.mode == "dist" and self.rank == 0:
             self.transport.broadcast_object(("stop",), src=0)
+            self._close_dist()
+
+    def _close_dist(self) -> None:
+        """Orderly teardown: every rank reaches the barrier before any process
+        group is destroyed, so no rank exits while a peer still has a gloo /
+        RCCL connection open to it."""
+        import torch.distributed as dist
+
+        self.transport.barrier()
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
     # ------------------------------------------------------------------
     def make_round(self, prompts: List[List[int]], params: List[SamplingParams], slots: List[int],

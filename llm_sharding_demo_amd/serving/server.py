@@ -168,7 +168,7 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
         ok = engine.healthy if engine is not None else True
         body = {"status": "ok" if ok else "unhealthy", "role": role, "model": mc.name}
         if engine is not None:
-            body.update(stages=engine.P, plan=engine.plan, mode=engine.mode,
+            body.update(stages=engine.P, plan=engine.plan, unit_plan=engine.unit_plan, mode=engine.mode,
                         devices=[str(d) for d in engine.devices])
             if not ok:
                 body["error"] = engine.last_error

@@ -170,3 +170,53 @@ def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp):
     out, out2 = json.loads(line[len("RESULT "):])
     assert out == golden
     assert out2 == golden[:2]
+
+
+# ---------------------------------------------------------------------------
+# Half-layer (unit) partitioning: a stage boundary between a layer's attention
+# and MLP halves must reproduce the unsplit model exactly.
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def golden_llama():
+    eng = Engine(EngineConfig(model_id="llama-test", num_stages=1, max_batch=8, device="cpu"))
+    return eng.generate_ids(PROMPTS, SamplingParams(greedy=True, max_new_tokens=5))
+
+
+@settings(max_examples=8, deadline=None)
+@given(st.lists(st.integers(1, 7), min_size=1, max_size=3, unique=True))
+def test_any_half_layer_partition_matches_unsplit(golden, cuts):
+    units = sorted(cuts)  # gpt2-test: 4 layers = 8 units, cut points in 1..7
+    cfg = EngineConfig(model_id="gpt2-test", num_stages=len(units) + 1, split_units=units,
+                       max_batch=8, device="cpu")
+    eng = Engine(cfg)
+    assert eng.unit_plan[0][0] == 0 and eng.unit_plan[-1][1] == 8
+    out = eng.generate_ids(PROMPTS, SamplingParams(greedy=True, max_new_tokens=6))
+    assert out == golden
+
+
+def test_half_layer_partition_llama(golden_llama):
+    cfg = EngineConfig(model_id="llama-test", num_stages=3, split_units=[3, 5], max_batch=8,
+                       device="cpu")
+    eng = Engine(cfg)
+    # stage 1 runs layer 1's MLP half and layer 2's attention half
+    s1 = eng.stages[1]
+    assert (s1.unit_start, s1.unit_end) == (3, 5) and s1.kv_layers == [2]
+    assert "layers.1.mlp.gate_up.weight" in s1.w and "layers.1.self_attn.qkv.weight" not in s1.w
+    assert "layers.2.self_attn.qkv.weight" in s1.w and "layers.2.mlp.down_proj.weight" not in s1.w
+    out = eng.generate_ids(PROMPTS, SamplingParams(greedy=True, max_new_tokens=5))
+    assert out == golden_llama
+
+
+def test_unit_plan_beats_whole_layers_on_xl():
+    from llm_sharding_demo_amd.parallel.partition import make_unit_plan, unit_stage_costs
+
+    mc = get_model_config("gpt2-xl")
+    for P in (2, 4, 8):
+        half = make_unit_plan(mc, P, rows=128, avg_ctx=192)
+        whole = make_unit_plan(mc, P, rows=128, avg_ctx=192, half_layers=False)
+        assert all(a % 2 == 0 for a, _ in whole)
+        ch, cw = unit_stage_costs(mc, half), unit_stage_costs(mc, whole)
+        assert max(ch) <= max(cw) + 1e-9
+        assert sum(ch) / P / max(ch) > 0.93  # within 7 % of a perfect split
+    # SPLIT_AT-style explicit layer splits map to even unit boundaries
+    assert make_unit_plan(mc, 2, split_points=[20]) == [(0, 40), (40, 96)]
