@@ -234,6 +234,13 @@ class EngineConfig:
     shard_b_service: str = "llm-shard-b"
     shard_port: int = 5000
     transport: str = "auto"  # auto | nccl | gloo | local | http
+    # Serving (runtime/scheduler.py): concurrent /generate requests arriving
+    # within batch_window_ms share one pipeline round; a round running longer
+    # than round_timeout_s marks the engine unhealthy; an HTTP request waits at
+    # most request_timeout_s.
+    batch_window_ms: float = 2.0
+    round_timeout_s: float = 600.0
+    request_timeout_s: float = 900.0
 
     @property
     def model(self) -> ModelConfig:
@@ -257,6 +264,9 @@ class EngineConfig:
             weights=os.environ.get("WEIGHTS") or None,
             transport=_env("TRANSPORT", "auto"),
             dp_replicas=int(_env("DP_REPLICAS", "1") or 1),
+            batch_window_ms=float(_env("BATCH_WINDOW_MS", "2.0")),
+            round_timeout_s=float(_env("ROUND_TIMEOUT_S", "600")),
+            request_timeout_s=float(_env("REQUEST_TIMEOUT_S", "900")),
         )
         if cfg.split_points and cfg.num_stages == 1:
             cfg.num_stages = len(cfg.split_points) + 1

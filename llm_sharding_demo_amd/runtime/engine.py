@@ -80,6 +80,7 @@ class Engine:
         self._lock = threading.Lock()
         self.stats = {"requests": 0, "tokens": 0, "rounds": 0, "busy_s": 0.0}
         self.last_round: Optional[RoundResult] = None
+        self.round_started: Optional[float] = None  # monotonic start of the running round (watchdog)
         self.max_seq = min(cfg.max_seq_len, self.mcfg.max_positions)
 
         if mode == "local":
@@ -249,7 +250,11 @@ class Engine:
                                              slots[j], microbatches, record_timing=record_timing)
                              if part else None for j, part in enumerate(parts)]
                     t0 = time.perf_counter()
-                    results = self._run_rounds(specs)
+                    self.round_started = time.monotonic()
+                    try:
+                        results = self._run_rounds(specs)
+                    finally:
+                        self.round_started = None
                     self.stats["busy_s"] += time.perf_counter() - t0
                     self.last_round = results[0]
                 except Exception as e:

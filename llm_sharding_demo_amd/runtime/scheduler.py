@@ -1,0 +1,199 @@
+"""Request scheduling in front of the pipeline engine: a batching request
+queue and a round watchdog.
+
+Reference behaviour (`server.py:154-210`): every /generate
+runs its own decode loop in FastAPI's threadpool; concurrent requests share
+nothing and each pays the full per-token HTTP round trips (measured: 4
+concurrent requests -> 0.83 tok/s aggregate vs 0.69 for one).
+
+Here concurrent requests are coalesced into pipeline rounds:
+
+* `RequestBatcher` -- one scheduler thread owns the engine.  Callers enqueue a
+  request and block on its completion; the scheduler takes the first waiting
+  request, keeps collecting for up to `window_ms` (or until the engine's
+  batch capacity is reached), then runs ONE round for the whole group: every
+  request is a sequence of that round's microbatches, so the pipeline stages
+  see a full batch instead of B = 1 (quirk Q12).  Requests with very
+  different lengths are split into separate rounds (a round runs
+  max(max_new_tokens) steps for all its sequences).
+* `Watchdog` -- a per-round deadline: if a round (a hung
+  RCCL peer, a dead stage) runs past `round_timeout_s`, the engine is marked
+  unhealthy with a clear error, /health reports it, and the waiting requests
+  fail instead of hanging forever.
+"""
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from ..config import SamplingParams
+
+log = logging.getLogger("llm_sharding_demo_amd.scheduler")
+
+
+class RequestTimeout(RuntimeError):
+    pass
+
+
+@dataclass
+class Request:
+    prompt_ids: List[int]
+    params: SamplingParams
+    t_submit: float = field(default_factory=time.monotonic)
+    t_start: float = 0.0
+    t_done: float = 0.0
+    output: Optional[List[int]] = None
+    error: Optional[BaseException] = None
+    _done: threading.Event = field(default_factory=threading.Event)
+
+    def wait(self, timeout: Optional[float] = None) -> List[int]:
+        if not self._done.wait(timeout):
+            raise RequestTimeout(f"request not finished after {timeout} s")
+        if self.error is not None:
+            raise self.error
+        return self.output
+
+    @property
+    def done(self) -> bool:
+        return self._done.is_set()
+
+
+class RequestBatcher:
+    """Coalesce concurrent generate requests into pipeline rounds."""
+
+    def __init__(self, engine, window_ms: float = 2.0, max_batch: Optional[int] = None,
+                 length_ratio: float = 4.0):
+        self.engine = engine
+        self.window = window_ms / 1e3
+        # whole capacity of the engine: KV slots x pipeline replicas
+        cap = engine.slots.capacity * max(1, getattr(engine, "R", 1))
+        self.max_batch = min(max_batch or cap, cap)
+        self.length_ratio = length_ratio
+        self._q: "queue.Queue[Optional[Request]]" = queue.Queue()
+        self._stop = threading.Event()
+        self.stats = {"batches": 0, "requests": 0, "max_batch_seen": 0}
+        self._thread = threading.Thread(target=self._loop, name="lsd-batcher", daemon=True)
+        self._thread.start()
+
+    # ------------------------------------------------------------------
+    def submit(self, prompt_ids: List[int], params: SamplingParams) -> Request:
+        if self._stop.is_set():
+            raise RuntimeError("batcher is closed")
+        if not self.engine.healthy:  # fail fast: the scheduler may be stuck in a dead round
+            raise RuntimeError(f"engine unhealthy: {self.engine.last_error}")
+        params.validate()
+        req = Request(list(prompt_ids), params)
+        self._q.put(req)
+        return req
+
+    def generate(self, prompt_ids: List[int], params: SamplingParams,
+                 timeout: Optional[float] = None) -> List[int]:
+        return self.submit(prompt_ids, params).wait(timeout)
+
+    @property
+    def queue_depth(self) -> int:
+        return self._q.qsize()
+
+    def close(self) -> None:
+        self._stop.set()
+        self._q.put(None)
+        self._thread.join(timeout=5)
+
+    # ------------------------------------------------------------------
+    def _collect(self, first: Request) -> List[Request]:
+        batch = [first]
+        deadline = time.monotonic() + self.window
+        while len(batch) < self.max_batch:
+            left = deadline - time.monotonic()
+            try:
+                r = self._q.get(timeout=max(left, 0.0)) if left > 0 else self._q.get_nowait()
+            except queue.Empty:
+                break
+            if r is None:
+                self._stop.set()
+                break
+            batch.append(r)
+        return batch
+
+    def _groups(self, batch: List[Request]) -> List[List[Request]]:
+        """Split by generation length so short requests do not ride out a long
+        round (a round runs max(max_new_tokens) steps for every sequence)."""
+        batch = sorted(batch, key=lambda r: r.params.max_new_tokens)
+        groups: List[List[Request]] = []
+        for r in batch:
+            n = max(1, r.params.max_new_tokens)
+            if groups and n <= self.length_ratio * max(1, groups[-1][0].params.max_new_tokens):
+                groups[-1].append(r)
+            else:
+                groups.append([r])
+        return groups
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            first = self._q.get()
+            if first is None:
+                break
+            batch = self._collect(first)
+            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(batch))
+            for group in self._groups(batch):
+                t0 = time.monotonic()
+                for r in group:
+                    r.t_start = t0
+                try:
+                    outs = self.engine.generate_ids([r.prompt_ids for r in group],
+                                                     [r.params for r in group])
+                    for r, o in zip(group, outs):
+                        r.output = o
+                except BaseException as e:  # fail the whole group, keep serving
+                    log.error("round failed: %s", e)
+                    for r in group:
+                        r.error = e
+                t1 = time.monotonic()
+                for r in group:
+                    r.t_done = t1
+                    r._done.set()
+                self.stats["batches"] += 1
+                self.stats["requests"] += len(group)
+        # fail whatever is still queued
+        while True:
+            try:
+                r = self._q.get_nowait()
+            except queue.Empty:
+                break
+            if r is not None:
+                r.error = RuntimeError("batcher closed")
+                r._done.set()
+
+
+class Watchdog:
+    """Marks the engine unhealthy when a round outlives its deadline."""
+
+    def __init__(self, engine, round_timeout_s: float, poll_s: float = 0.25):
+        self.engine = engine
+        self.timeout = round_timeout_s
+        self.poll = poll_s
+        self.fired = False
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._loop, name="lsd-watchdog", daemon=True)
+        self._thread.start()
+
+    def _loop(self) -> None:
+        while not self._stop.wait(self.poll):
+            started = getattr(self.engine, "round_started", None)
+            if started is None or self.fired:
+                continue
+            elapsed = time.monotonic() - started
+            if elapsed > self.timeout:
+                self.fired = True
+                msg = f"round exceeded its {self.timeout:.0f} s deadline (running {elapsed:.0f} s)"
+                log.error("watchdog: %s; marking engine unhealthy", msg)
+                self.engine.healthy = False
+                self.engine.last_error = f"WatchdogTimeout: {msg}"
+
+    def close(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=5)

@@ -17,7 +17,9 @@ Roles (env SHARD_ROLE, `server.py:21`):
 Additions: optional sampling fields on /generate (temperature, top_k, greedy,
 seed, stop_at_eos; defaults = reference sampler), 422 on empty/over-long
 prompts (instead of the reference's 500, quirk Q9), GET /health, GET /metrics
-(Prometheus text).
+(Prometheus text).  Concurrent /generate calls are batched into shared
+pipeline rounds by runtime/scheduler.py's RequestBatcher; a round watchdog
+turns a hung pipeline into 503s instead of hanging requests.
 """
 from __future__ import annotations
 
@@ -96,6 +98,13 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
     metrics = Metrics()
     app = FastAPI(title="llm-sharding-demo (MI355X)")
     app.state.engine, app.state.shard, app.state.metrics = engine, shard, metrics
+    batcher = watchdog = None
+    if engine is not None:
+        from ..runtime.scheduler import RequestBatcher, Watchdog
+
+        batcher = RequestBatcher(engine, window_ms=cfg.batch_window_ms)
+        watchdog = Watchdog(engine, cfg.round_timeout_s)
+    app.state.batcher, app.state.watchdog = batcher, watchdog
 
     def _role_is(*roles):
         return role in roles or role == "all"
@@ -149,14 +158,25 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
         if not ids:
             raise HTTPException(422, "prompt must encode to at least one token")
         t0 = time.perf_counter()
+        from ..runtime.scheduler import RequestTimeout
+
         try:
             sp.validate()
             if engine is not None:
-                out = engine.generate_ids([ids], [sp])[0]
+                if len(ids) + sp.max_new_tokens > engine.max_seq:
+                    raise ValueError(f"prompt ({len(ids)}) + max_new_tokens ({sp.max_new_tokens}) "
+                                     f"exceeds the context limit {engine.max_seq}")
+                out = batcher.generate(ids, sp, timeout=cfg.request_timeout_s)
             else:
                 out = http_generate(cfg, ids, sp)
         except ValueError as e:
             raise HTTPException(422, str(e))
+        except RequestTimeout as e:
+            raise HTTPException(504, str(e))
+        except RuntimeError as e:
+            if engine is not None and not engine.healthy:
+                raise HTTPException(503, f"engine unhealthy: {engine.last_error}")
+            raise
         dt = time.perf_counter() - t0
         metrics.observe_request(len(out), dt)
         if engine is not None and engine.last_round is not None and engine.last_round.step_times_ms:
@@ -184,7 +204,11 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
             extra = {"engine_healthy": 1 if engine.healthy else 0,
                      "engine_stages": engine.P,
                      "kv_slots_free": engine.slots.available,
-                     "kv_slots_total": engine.slots.capacity}
+                     "kv_slots_total": engine.slots.capacity,
+                     "queue_depth": batcher.queue_depth,
+                     "batched_rounds_total": batcher.stats["batches"],
+                     "batched_requests_total": batcher.stats["requests"],
+                     "max_batch_seen": batcher.stats["max_batch_seen"]}
         return metrics.render(extra)
 
     return app
