@@ -208,14 +208,18 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
 // GELU, residual add) works with any split and no extra launch is needed.
 // 32-k MFMA steps per round: 16 (512 k) up to M = 64; 8 (256 k) for M <= 128
 // so the A image stays at 64 KiB (2 blocks / CU) while the rows double.
+// Rounds are double-buffered (2 LDS images): 4 steps (128 k) above 64 rows,
+// 8 up to 64 rows, 16 up to 32 rows keep both images at <= 64 KiB (2 blocks/CU).
 template <int MT>
 constexpr int sk_round_steps() {
 #ifdef LSD_SK_ROUND
   return LSD_SK_ROUND;
 #else
-  return MT > 4 ? 8 : 16;
+  return MT > 4 ? 4 : (MT > 2 ? 8 : 16);
 #endif
 }
+// s_waitcnt simm16 (gfx9 layout) for lgkmcnt(0) alone
+constexpr int LGKM0_SK = 0xC07F;
 
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)g,
@@ -237,8 +241,8 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
   constexpr int BNB = 64 * NW;             // block tile columns
   constexpr int SK_ROUND_STEPS = sk_round_steps<MT>();
   constexpr int NCHUNK = SK_ROUND_STEPS / 4;
-  __shared__ __attribute__((aligned(16))) char smem[NCHUNK * CHUNK_BYTES + 16];
-  int* s_flag = reinterpret_cast<int*>(smem + NCHUNK * CHUNK_BYTES);
+  __shared__ __attribute__((aligned(16))) char smem[2 * NCHUNK * CHUNK_BYTES + 16];
+  int* s_flag = reinterpret_cast<int*>(smem + 2 * NCHUNK * CHUNK_BYTES);
 
   LSD_STAMP(0)
   if (p.stamps && threadIdx.x == 0)
@@ -267,34 +271,50 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
 #pragma unroll
     for (int ns = 0; ns < NW; ++ns) acc[mt][ns] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = kb; k0 < ke; k0 += SK_ROUND_STEPS) {
+  // Double-buffered rounds: round r+1's W fragments (second register set) and
+  // A image (second LDS buffer) are issued BEFORE round r's MFMAs, so a split
+  // with several rounds pays one HBM latency instead of one per round.  Every
+  // round issues the same number of loads per thread (partial rounds re-load
+  // clamped addresses), so "round r has landed" is the counted wait
+  // vmcnt(LOADS) -- raw s_barrier, never __syncthreads (it would drain the
+  // next round's LDS-DMA too: guide §5 "Pipelining across barriers").
+  constexpr int LOADS = SK_ROUND_STEPS * NW + NCHUNK * MT;  // per thread per round
+  static_assert(LOADS <= 63, "vmcnt holds at most 63 outstanding loads");
+  constexpr int WAIT_PREV = (LOADS & 0xF) | ((LOADS >> 4) << 14) | (0x7 << 4) | (0xF << 8);
+  constexpr int WAIT_ALL = (0x7 << 4) | (0xF << 8);  // vmcnt(0)
+  constexpr int BUF_BYTES = NCHUNK * CHUNK_BYTES;
+  const int nrounds = (ke - kb + SK_ROUND_STEPS - 1) / SK_ROUND_STEPS;
+
+  auto issue = [&](int rd, bf16x8 (&wv)[SK_ROUND_STEPS][NW], char* buf) {
+    const int k0 = kb + rd * SK_ROUND_STEPS;
     const int nst = min(SK_ROUND_STEPS, ke - k0);
-    const int nch = (nst + 3) >> 2;
-    // All W fragments of the round are issued back to back.  No per-load guard:
-    // a runtime "if (j < nst) load" makes hipcc branch around each load and
-    // wait vmcnt(0) per element (guide §5 trap (c)); steps past the round end
-    // re-load the last valid step and are never consumed.
-    bf16x8 wv[SK_ROUND_STEPS][NW];
+    // No per-load guard: a runtime "if (j < nst) load" makes hipcc branch
+    // around each load and wait vmcnt(0) per element (guide §5 trap (c));
+    // steps past the round end re-load the last valid step, never consumed.
 #pragma unroll
     for (int j = 0; j < SK_ROUND_STEPS; ++j)
 #pragma unroll
       for (int ns = 0; ns < NW; ++ns) wv[j][ns] = ld8(wrow[ns] + (long)(k0 + min(j, nst - 1)) * 32);
-    // A chunks (issued after W: the HBM-latency loads go first, the L2-resident
-    // activations overlap them): MT*4 wave-instructions (1 KiB = 4 rows of 256 B) per chunk
-    for (int inst = w; inst < nch * MT * 4; inst += 4) {
+    // A chunks (after W: the HBM-latency loads go first, the L2-resident
+    // activations overlap them): MT*4 wave-instructions (1 KiB = 4 rows of
+    // 256 B) per chunk; chunks past the round end re-load a valid chunk
+#pragma unroll
+    for (int i = 0; i < NCHUNK * MT; ++i) {
+      const int inst = w + 4 * i;
       const int c = inst / (MT * 4), q = inst % (MT * 4);
       const int row = q * 4 + (lane >> 4);
       const int lch = (lane & 15) ^ (row & 15);
-      const int kk = min((k0 + c * 4) * 32 + lch * 8, p.K - 8);
-      glds16(p.A + (long)min(rb0 + row, p.M - 1) * p.lda + kk, smem + c * CHUNK_BYTES + q * 1024);
+      const int kk = min((k0 + min(c * 4, nst - 1)) * 32 + lch * 8, p.K - 8);
+      glds16(p.A + (long)min(rb0 + row, p.M - 1) * p.lda + kk, buf + c * CHUNK_BYTES + q * 1024);
     }
-    __syncthreads();  // vmcnt(0): the A image and this wave's W fragments have landed
-    if (k0 == kb) { LSD_STAMP(1) }
-    // A fragments come from LDS one step ahead of the MFMAs that use them, so
-    // the ds_read latency of step j+1 hides under step j's MFMAs for any round
-    // length (the round count nst is wave-uniform).
+  };
+  // A fragments come from LDS one step ahead of the MFMAs that use them, so
+  // the ds_read latency of step j+1 hides under step j's MFMAs for any round
+  // length (the round count nst is wave-uniform).
+  auto compute = [&](int rd, bf16x8 (&wv)[SK_ROUND_STEPS][NW], const char* buf) {
+    const int nst = min(SK_ROUND_STEPS, ke - (kb + rd * SK_ROUND_STEPS));
     auto read_a = [&](int j, bf16x8 (&a)[MT]) {
-      const char* img = smem + (j >> 2) * CHUNK_BYTES;
+      const char* img = buf + (j >> 2) * CHUNK_BYTES;
       const int lch = (j & 3) * 4 + g;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -325,7 +345,41 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) a_cur[mt] = a_nxt[mt];
     }
-    __syncthreads();  // the image is rewritten by the next round
+    // every wave's reads of `buf` retire before anyone re-fills it
+    __builtin_amdgcn_s_waitcnt(LGKM0_SK);
+    __builtin_amdgcn_s_barrier();
+  };
+  // round rd with round rd+1 issued first (straight-line, so hipcc's own
+  // register waits count exactly like the explicit one)
+  auto body_more = [&](int rd, bf16x8 (&cur)[SK_ROUND_STEPS][NW], char* cbuf,
+                       bf16x8 (&nxt)[SK_ROUND_STEPS][NW], char* nbuf) {
+    issue(rd + 1, nxt, nbuf);
+    __builtin_amdgcn_s_waitcnt(WAIT_PREV);  // this thread's round-rd loads landed
+    __builtin_amdgcn_s_barrier();           // ... and every other wave's A DMA
+    if (rd == 0) { LSD_STAMP(1) }
+    compute(rd, cur, cbuf);
+  };
+  auto body_last = [&](int rd, bf16x8 (&cur)[SK_ROUND_STEPS][NW], char* cbuf) {
+    __builtin_amdgcn_s_waitcnt(WAIT_ALL);
+    __builtin_amdgcn_s_barrier();
+    if (rd == 0) { LSD_STAMP(1) }
+    compute(rd, cur, cbuf);
+  };
+
+  bf16x8 wv0[SK_ROUND_STEPS][NW], wv1[SK_ROUND_STEPS][NW];
+  char* buf0 = smem;
+  char* buf1 = smem + BUF_BYTES;
+  int rd = 0;
+  if (nrounds > 0) issue(0, wv0, buf0);
+  for (; rd + 2 < nrounds; rd += 2) {
+    body_more(rd, wv0, buf0, wv1, buf1);
+    body_more(rd + 1, wv1, buf1, wv0, buf0);
+  }
+  if (nrounds - rd == 2) {
+    body_more(rd, wv0, buf0, wv1, buf1);
+    body_last(rd + 1, wv1, buf1);
+  } else if (nrounds - rd == 1) {
+    body_last(rd, wv0, buf0);
   }
   LSD_STAMP(2)
 
