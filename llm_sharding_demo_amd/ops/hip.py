@@ -234,6 +234,12 @@ class HipBackend(Backend):
             r.pending.append((slab, b))
 
     def logits(self, xn, w):
+        # vocab-wide N: the 128x128 LDS-tiled kernel fills the chip without
+        # split-K and reads the activation rows once per 128 columns instead
+        # of once per 64 -- measured 41.8 vs 64.2 us at M = 128 (GPT-2 XL),
+        # 222.7 vs 300.3 us for Llama-3 8B (tools/microbench.py lmhead)
+        if w.shape[0] >= 16384 and w.shape[1] % 64 == 0:
+            return self.C.linear_f32(xn, w, True, 1, self.counters)
         tiled, splits = self._gemm_kw(xn.shape[0], w.shape[0], w.shape[1])
         return self.C.linear_f32(xn, w, tiled, splits, self.counters)
 

@@ -122,16 +122,18 @@ def make_plan(cfg: ModelConfig, num_stages: int, split_points: Optional[Sequence
 # calibrated against the kernel profile and microbenchmarks of the bench
 # config (profiles/r1_xl_*_kernel_stats.csv, r1_microbench_*; 128-row
 # microbatches, GPT-2 XL: attention half ~70 us, MLP half ~47 us, head ~146 us):
-#   decode GEMM  ~ 5 us + weight bytes / 1.3 TB/s (N < 16k; 2.3 TB/s for
-#                lm_head) + FLOPs / 2 PF; QKV + 6 us (KV-cache scatter, RoPE)
+#   decode GEMM  ~ 5 us + weight bytes / 1.3 TB/s + FLOPs / 2 PF; QKV + 6 us
+#                (KV-cache scatter, RoPE); lm_head (tiled kernel) 5 us +
+#                bytes / 4.4 TB/s
 #   attention    ~ 3 us + KV bytes / 6 TB/s
 #   norm 6 us, sampler 8 us + 0.37 us/row, embed 4 us.
 UnitPlan = List[Tuple[int, int]]
 
 
 def _gemm_us(n: int, k: int, rows: int) -> float:
-    bw = 2.3e6 if n >= 16384 else 1.3e6  # bytes per us
-    return 5.0 + n * k * 2 / bw + 2.0 * rows * n * k / 2.0e9
+    if n >= 16384:  # vocab projection on the 128x128 tiled kernel
+        return 5.0 + n * k * 2 / 4.4e6
+    return 5.0 + n * k * 2 / 1.3e6 + 2.0 * rows * n * k / 2.0e9  # bytes, FLOPs per us
 
 
 def unit_costs(cfg: ModelConfig, rows: int = 128, avg_ctx: int = 192) -> Tuple[List[float], float, float]:

@@ -69,7 +69,7 @@ def report(name, us, nbytes, extra=None):
     print(json.dumps(row), flush=True)
 
 
-def bench_gemm(M, N, K, act=0, resid=False, label=""):
+def bench_gemm(M, N, K, act=0, resid=False, label="", force_tiled=False):
     ws = rotating(lambda: torch.randn(N, K, device=DEV).bfloat16(), N * K * 2)
     a = torch.randn(M, K, device=DEV).bfloat16()
     x = torch.randn(M, N, device=DEV)
@@ -79,8 +79,13 @@ def bench_gemm(M, N, K, act=0, resid=False, label=""):
     be.counters = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
     nw = 2 if act == 2 else 1
     tiled, splits = be._gemm_kw(M, N, K, nw)
+    if force_tiled:
+        tiled, splits = True, 1
     if resid:
         splits = be._resid_splits(M, N, K)
+        if force_tiled:  # the tiled path's own split rule at these M rows
+            tiles = math.ceil(M / 128) * math.ceil(N / 128)
+            splits = max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
 
     def run():
         w = ws[it[0] % len(ws)]
@@ -282,6 +287,17 @@ def main():
                     bench_gemm(128, H, F, resid=True, label="_proj2" + tag)
                     bench_gemm(128, V, H, label="_lmhead" + tag)
         HipBackend.SK_ROWS, HipBackend.SK_TARGET, HipBackend.NW2_ROWS = 64, 384, 64
+    if "lmhead" in which:  # vocab projection: decode kernel vs 128x128 tiled kernel
+        for M in (16, 32, 64, 128):
+            bench_gemm(M, V, H, label="_lmhead")
+            bench_gemm(M, V, H, label="_lmhead_tiled", force_tiled=True)
+        bench_gemm(128, 128256, 4096, label="_lmhead_llama")
+        bench_gemm(128, 128256, 4096, label="_lmhead_llama_tiled", force_tiled=True)
+    if "tiledsk" in which:  # split-K slabs + norm combine: decode kernel vs 128x128 tiled
+        for M in (64, 128):
+            for (N, K, nm) in ((3 * H, H, "qkv"), (F, H, "fc"), (H, H, "proj"), (H, F, "proj2")):
+                bench_gemm(M, N, K, resid=True, label=f"_resid_{nm}")
+                bench_gemm(M, N, K, resid=True, label=f"_resid_{nm}_tiled", force_tiled=True)
     if "gemm" in which:
         for M in (1, 16, 32, 64, 128, 256):
             bench_gemm(M, 3 * H, H, label="_qkv")
