@@ -50,6 +50,17 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __rest
                                                    int H, float eps, const int* __restrict__ rows) {
   __shared__ float red[16];
   const int t = blockIdx.x;
+  // gamma / beta are issued first: their latency overlaps the row loads
+  // instead of adding a second memory round trip after the reductions
+  bf16x4 wv[MAXV], bv[MAXV];
+  if (out != nullptr) {
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = min((threadIdx.x + i * 256) * 4, H - 4);
+      wv[i] = ld4(w + c);
+      if (!RMS) bv[i] = ld4(b + c);
+    }
+  }
   const int src = rows ? rows[t] : t;  // optional row gather (last-token rows)
   float* xr = x + (long)src * H;
   f32x4 v[MAXV];
@@ -92,13 +103,12 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __rest
   for (int i = 0; i < MAXV; ++i) {
     const int c = (threadIdx.x + i * 256) * 4;
     if (c < H) {
-      bf16x4 ww = ld4(w + c);
       f32x4 y = (v[i] - mean) * rstd;
       bf16x4 r;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float z = y[j] * bf2f(ww[j]);
-        if (!RMS) z += bf2f(b[c + j]);
+        float z = y[j] * bf2f(wv[i][j]);
+        if (!RMS) z += bf2f(bv[i][j]);
         r[j] = f2bf(z);
       }
       st4(o + c, r);
