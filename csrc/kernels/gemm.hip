@@ -450,17 +450,42 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
   }
   LSD_STAMP(4)
 
+  // Epilogue through LDS (free: the last round ended with every DMA drained
+  // and a barrier): the MFMA layout gives a lane 4 rows x 1 column, i.e.
+  // 2-4-byte stores scattered over 4 rows (KV-cache scatter, bf16 outputs,
+  // slabs); transposed through an fp32 [ROWS][BNB] tile, every store is a
+  // row-contiguous 16-byte vector (epilogue8, as in the tiled kernels).
+  constexpr int CLD = BNB + 4;  // row stride: 4 rows x 16 columns hit 64 distinct banks
+  constexpr bool LDS_EPI = EPI != EPI_SILU_MUL && ROWS * CLD * 4 <= 2 * NCHUNK * CHUNK_BYTES;
+  if constexpr (LDS_EPI) {
+    float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row0 = rb0 + mt * 16 + 4 * g;
-    if constexpr (EPI == EPI_SILU_MUL) {
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int ns = 0; ns < NW; ns += 2)
-        epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns + 1], 0);
-    } else {
+      for (int ns = 0; ns < NW; ++ns)
 #pragma unroll
-      for (int ns = 0; ns < NW; ++ns)  // 16-column sub-tiles past N: wave-uniform skip
-        if (n_w + 16 * ns < p.N) epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns], split);
+        for (int q = 0; q < 4; ++q)
+          ct[(mt * 16 + 4 * g + q) * CLD + w * 16 * NW + ns * 16 + r] = acc[mt][ns][q];
+    __syncthreads();
+    const int n0 = tile * BNB;
+    for (int c = threadIdx.x; c < ROWS * (BNB / 8); c += 256) {
+      const int row = c / (BNB / 8), ch = c % (BNB / 8);
+      const int m = rb0 + row, n = n0 + ch * 8;
+      if (m < p.M && n < p.N) epilogue8<EPI>(p, m, n, ct + row * CLD + ch * 8, split);
+    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row0 = rb0 + mt * 16 + 4 * g;
+      if constexpr (EPI == EPI_SILU_MUL) {
+#pragma unroll
+        for (int ns = 0; ns < NW; ns += 2)
+          epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns + 1], 0);
+      } else {
+#pragma unroll
+        for (int ns = 0; ns < NW; ++ns)  // 16-column sub-tiles past N: wave-uniform skip
+          if (n_w + 16 * ns < p.N) epilogue4<EPI>(p, row0, n_w + 16 * ns + r, acc[mt][ns], acc[mt][ns], split);
+      }
     }
   }
   LSD_STAMP(5)
