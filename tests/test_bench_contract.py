@@ -21,7 +21,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("n,dp", [(1, 1), (2, 1), (4, 2)])
+@pytest.mark.parametrize("n,dp", [(1, 1), (2, 1), (4, 2), (8, 1)])
 def test_bench_json_contract(n, dp):
     args = ["--gpus", str(n), "--dp", str(dp), "--device", "cpu", "--transport", "gloo",
             "--model", "gpt2-test", "--batch", "2", "--prompt", "4", "--gen", "3",
