@@ -101,6 +101,27 @@ def test_linear_residual_and_f32(C, CNT, M, splits, defer):
     close(C.linear_f32(a, w, tiled, 1 if tiled else splits, CNT), ref.linear(a, w), 2e-3, 1e-3)
 
 
+@pytest.mark.parametrize("M", [1, 40, 128])
+def test_decode_gemm_wide_partial_tiles(C, CNT, M):
+    """128-column decode tiles (NW = 2) with a masked partial last tile
+    (N = 320 = 2.5 tiles): plain, GELU, split-K residual and fp32 epilogues."""
+    C.gemm_set_nw2_rows(0)
+    try:
+        N, K = 320, 512
+        a, w, bias = bf(M, K, seed=40), bf(N, K, scale=0.05, seed=41), bf(N, scale=0.1, seed=42)
+        assert C.gemm_sk_nw(M, 0) == 2
+        for sp in (1, 3):
+            close(C.linear(a, w, bias, 1, False, sp, CNT), ref.gelu_new(ref.linear(a, w, bias)), 3e-2)
+            close(C.linear_f32(a, w, False, sp, CNT), ref.linear(a, w), 2e-3, 1e-3)
+            x = torch.randn(M, N, device=DEV)
+            x_ref = x + ref.linear(a, w, bias)
+            C.linear_residual(a, w, bias, x, sp, False, CNT, False)
+            close(x, x_ref, 2e-3, 1e-3)
+        assert int(CNT.abs().sum()) == 0
+    finally:
+        C.gemm_set_nw2_rows(1 << 30)
+
+
 def test_split_k_deterministic(C, CNT):
     a, w = bf(64, 1600, seed=30), bf(4800, 1600, scale=0.03, seed=31)
     y1 = C.linear(a, w, None, 0, False, 7, CNT)
