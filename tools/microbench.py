@@ -150,6 +150,61 @@ def bench_prefill_gemms(T, H, F, nh, hd, label=""):
                 "hipblaslt_TFLOP/s": round(fl / ut / 1e6, 1)})
 
 
+def bench_decode_layer(M, H=1600, F=6400, nh=25, hd=64, ctx=192, slots=256):
+    """One GPT-2 XL decode layer's kernels at M rows, in engine order with
+    their real epilogues (QKV scatter into a ctx-deep cache, deferred residual
+    slabs + norm combine), each timed alone and the chain as one graph, on
+    rotating weight copies (cold in the 256 MiB Infinity Cache)."""
+    from llm_sharding_demo_amd.ops.hip import HipBackend
+    from llm_sharding_demo_amd.ops import Residual
+
+    be = HipBackend()
+    be.counters = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    nl = 6  # weight copies: 6 x 61 MB > MALL
+    W = [dict(wq=torch.randn(3 * H, H, device=DEV).bfloat16() * 0.02,
+              bq=torch.zeros(3 * H, device=DEV).bfloat16(),
+              wp=torch.randn(H, H, device=DEV).bfloat16() * 0.02,
+              wf=torch.randn(F, H, device=DEV).bfloat16() * 0.02,
+              bfc=torch.zeros(F, device=DEV).bfloat16(),
+              wp2=torch.randn(H, F, device=DEV).bfloat16() * 0.02) for _ in range(nl)]
+    g1 = torch.ones(H, device=DEV).bfloat16()
+    b1 = torch.zeros(H, device=DEV).bfloat16()
+    kc = torch.zeros(slots, nh, ctx + 8, hd, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    sl = torch.arange(M, dtype=torch.int32, device=DEV)
+    pos = torch.full((M,), ctx, dtype=torch.int32, device=DEV)
+    x = torch.randn(M, H, device=DEV)
+    it = [0]
+
+    class Meta:
+        is_decode, num_seqs, max_ctx = True, M, ctx + 1
+        seq_slots, token_pos, token_slots = sl, pos, sl
+
+    def layer(parts):
+        w = W[it[0] % nl]
+        it[0] += 1
+        r = Residual(x)
+        xn = be.layernorm(r, g1, b1, 1e-5)
+        if "qkv" in parts or "all" in parts:
+            q = C.linear_qkv(xn, w["wq"], w["bq"], kc, vc, sl, pos, H, H, hd, None, False,
+                             be._sk_splits(M, 3 * H, H), be.counters)
+        else:
+            q = torch.empty(M, H, device=DEV).bfloat16()
+        o = be.attention(q, kc, vc, Meta) if ("attn" in parts or "all" in parts) else q
+        be.linear_residual(o, w["wp"], None, r)
+        xn = be.layernorm(r, g1, b1, 1e-5)
+        h = be.linear(xn, w["wf"], w["bfc"], act="gelu")
+        be.linear_residual(h, w["wp2"], None, r)
+        be.flush(r)
+
+    us = timeit(lambda: layer(("all",)), iters=12)
+    report(f"decode_layer M={M} (norm,qkv,attn,proj,norm,fc,proj2) ctx={ctx}", us, 61e6 + M * ctx * 6400)
+    us = timeit(lambda: layer(("attn",)), iters=12)
+    report(f"decode_layer_no_qkv M={M}", us, 0)
+    us = timeit(lambda: layer(("qkv",)), iters=12)
+    report(f"decode_layer_no_attn M={M}", us, 0)
+
+
 def bench_resid_norm(M, N, K, splits_list, label=""):
     """Residual GEMM + the following LayerNorm, two ways: split-K combined in
     the GEMM (last arriver) vs deferred slabs combined by the norm kernel."""
@@ -287,6 +342,9 @@ def main():
                     bench_gemm(128, H, F, resid=True, label="_proj2" + tag)
                     bench_gemm(128, V, H, label="_lmhead" + tag)
         HipBackend.SK_ROWS, HipBackend.SK_TARGET, HipBackend.NW2_ROWS = 64, 384, 64
+    if "layer" in which:
+        for M in (1, 16, 64, 128):
+            bench_decode_layer(M)
     if "lmhead" in which:  # vocab projection: decode kernel vs 128x128 tiled kernel
         for M in (16, 32, 64, 128):
             bench_gemm(M, V, H, label="_lmhead")
