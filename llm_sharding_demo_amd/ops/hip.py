@@ -85,7 +85,11 @@ class HipBackend(Backend):
     # decode (split-K, last-arriver) GEMM up to this many rows; tiled above
     SK_MAX_M = int(os.environ.get("LSD_SK_MAX_M", "128"))
     DEFER_RESID = os.environ.get("LSD_DEFER_RESID", "1") == "1"
-    SK_TARGET = int(os.environ.get("LSD_SK_TARGET", "384"))
+    # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
+    # lanes running concurrently each GEMM should fill ~1/c of the chip so the
+    # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:
+    # 31.1k -> 32.1k tok/s, GPT-2 XL, 2 x 128 rows).  LSD_SK_TARGET overrides.
+    SK_TARGET = int(os.environ.get("LSD_SK_TARGET", "0")) or None
     SK_MIN_STEPS = int(os.environ.get("LSD_SK_MIN_STEPS", "2"))  # 32-k steps per split
     # decode GEMM rows per row block when an under-filled grid (deferred
     # residual projections) is split into row blocks (sk_rblocks in gemm.hip)
@@ -100,6 +104,7 @@ class HipBackend(Backend):
         self.counters = None
         self._rope = None
         self.lane = 0  # microbatch lane (stream) currently being issued; see pipeline.py
+        self.concurrency = 1  # microbatch lanes running at once (set per round by the pipeline)
 
     # ------------------------------------------------------------------
     def prepare_stage(self, stage) -> None:
@@ -156,7 +161,8 @@ class HipBackend(Backend):
     def _sk_splits(self, M: int, N: int, K: int, nw: int = 1) -> int:
         nw = max(nw, 2 if M > self.NW2_ROWS else 1)  # mirrors sk_nw() in gemm.hip
         tiles = math.ceil(N / (64 * nw))  # >= SK_TARGET workgroups: never row-blocked
-        return max(1, min(math.ceil(self.SK_TARGET / tiles), K // 32 // self.SK_MIN_STEPS or 1))
+        target = self.SK_TARGET or max(128, 384 // max(1, self.concurrency))
+        return max(1, min(math.ceil(target / tiles), K // 32 // self.SK_MIN_STEPS or 1))
 
     def _gemm_kw(self, M: int, N: int, K: int, nw: int = 1):
         if self._tiled(M):

@@ -143,6 +143,8 @@ class StageWorker:
         L = max(1, len(self.lanes))
         for lane in self.lanes:
             lane.wait_stream(torch.cuda.current_stream(dev))
+        # kernels size their grids for the lanes that actually run side by side
+        st.backend.concurrency = min(L, M)
 
         def on_lane(m):
             if not self.lanes:

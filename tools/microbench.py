@@ -328,7 +328,7 @@ def main():
                 bench_gemm(M, H, H, resid=True, label="_proj")
                 bench_gemm(M, H, F, resid=True, label="_proj2")
                 bench_gemm(M, V, H, label="_lmhead")
-        HipBackend.SK_TARGET = 384
+        HipBackend.SK_TARGET = None
     if "rows" in which:  # decode GEMM: row blocks x column tile x split target at M = 128
         from llm_sharding_demo_amd.ops.hip import HipBackend
         for nw2 in (128, 64):
@@ -341,7 +341,7 @@ def main():
                     bench_gemm(128, H, H, resid=True, label="_proj" + tag)
                     bench_gemm(128, H, F, resid=True, label="_proj2" + tag)
                     bench_gemm(128, V, H, label="_lmhead" + tag)
-        HipBackend.SK_ROWS, HipBackend.SK_TARGET, HipBackend.NW2_ROWS = 64, 384, 64
+        HipBackend.SK_ROWS, HipBackend.SK_TARGET, HipBackend.NW2_ROWS = 64, None, 1 << 30
     if "layer" in which:
         for M in (1, 16, 64, 128):
             bench_decode_layer(M)
