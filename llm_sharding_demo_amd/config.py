@@ -239,6 +239,11 @@ class EngineConfig:
     # than round_timeout_s marks the engine unhealthy; an HTTP request waits at
     # most request_timeout_s.
     batch_window_ms: float = 2.0
+    # Chunked prefill: prompts are prefilled in steps of at most this many
+    # tokens per sequence (0 = whole prompt in one step).  Bounds prefill
+    # activation memory for long contexts and lets chunks of different
+    # microbatches pipeline across stages.
+    prefill_chunk: int = 0
     round_timeout_s: float = 600.0
     request_timeout_s: float = 900.0
 
@@ -265,6 +270,7 @@ class EngineConfig:
             transport=_env("TRANSPORT", "auto"),
             dp_replicas=int(_env("DP_REPLICAS", "1") or 1),
             batch_window_ms=float(_env("BATCH_WINDOW_MS", "2.0")),
+            prefill_chunk=int(_env("PREFILL_CHUNK", "0")),
             round_timeout_s=float(_env("ROUND_TIMEOUT_S", "600")),
             request_timeout_s=float(_env("REQUEST_TIMEOUT_S", "900")),
         )

@@ -114,10 +114,12 @@ class StageModel:
             return self.backend.embed(ids, meta.token_pos, self.w["wte"], self.w["wpe"])
         return self.backend.embed(ids, meta.token_pos, self.w["embed_tokens"], None)
 
-    def forward(self, meta: BatchMeta, inp: torch.Tensor, all_logits: bool = False) -> torch.Tensor:
+    def forward(self, meta: BatchMeta, inp: torch.Tensor, all_logits: bool = False,
+                head: bool = True) -> torch.Tensor:
         """inp: token ids int32 [T] (first stage) or hidden fp32 [T, H].
 
-        Returns hidden fp32 [T, H] (non-last stage) or fp32 logits
+        Returns hidden fp32 [T, H] (non-last stage, or `head=False`: a
+        non-final prefill chunk only fills the KV cache) or fp32 logits
         [B, vocab_padded] for the last query of each sequence (last stage;
         [T, vocab_padded] with all_logits)."""
         x = self.embed(inp, meta) if self.first else inp
@@ -132,7 +134,7 @@ class StageModel:
             else:
                 attn_fn(self._kv_index[i], i, r, meta)
         x = self.backend.flush(r)
-        if not self.last:
+        if not (self.last and head):
             return x
         return self.head(x, meta, all_logits)
 

@@ -7,22 +7,32 @@ host -- strictly sequentially, so one shard is always idle and each token
 costs two HTTP round trips.
 
 Here a generation *round* is a set of sequences split into M microbatches.
-Every stage runs the same static schedule:
+Every stage runs the same static schedule over items (step s, microbatch m):
 
-    for step in 0..G-1:            # step 0 = prefill, then one token per step
-        for mb in 0..M-1:
-            input  <- prompt ids (stage 0, step 0)
-                    | sampled ids of (step-1, mb) from stage P-1 (stage 0)
-                    | boundary hidden of (step, mb) from stage r-1
-            output <- this stage's layers  (+ ln_f, lm_head, sampler on P-1)
+    steps 0..C-1       prefill chunks (C = 1 unless the round asks for
+                       chunked prefill: each chunk carries up to `chunk`
+                       prompt tokens per sequence, aligned to the END of the
+                       prompt so the last chunk holds every sequence's last
+                       position)
+    steps C..C+G-2     decode, one token per sequence per step
+
+    for s in steps:
+        for m in 0..M-1:
+            input  <- prompt chunk s (stage 0, prefill)
+                    | sampled ids of (s-1, m) from stage P-1 (stage 0, decode)
+                    | boundary hidden of (s, m) from stage r-1
+            output <- this stage's units (+ ln_f, lm_head, sampler on P-1 for
+                      the last chunk and every decode step)
             send output -> stage r+1   (or token ids -> stage 0 from P-1)
 
 With M >= P microbatches every stage is busy in steady state (stage r works
 on microbatch (t - r) mod M at tick t).  Receives for the next item are
-posted before the current item's compute is enqueued, so the transfer
-overlaps compute; `Handle.wait()` only orders the compute stream behind the
-comm stream.  Decode steps (step >= 2) replay one hipGraph per microbatch:
-all positions / sampler counters advance on the device inside the graph.
+posted before the current item's compute is enqueued when they target a
+different buffer, so the transfer overlaps compute; `Handle.wait()` only
+orders the compute stream behind the comm stream.  Microbatch m runs on
+HIP stream lanes[m % L], so independent microbatches overlap on the GPU.
+Decode steps after the first replay one hipGraph per microbatch: positions
+and sampler counters advance on the device inside the graph.
 """
 from __future__ import annotations
 
@@ -31,7 +41,7 @@ import os
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -64,6 +74,7 @@ class RoundSpec:
     steps: int  # tokens generated per sequence (>= 1)
     use_graphs: bool = True
     record_timing: bool = False
+    prefill_chunk: int = 0  # prompt tokens per sequence per prefill step; 0 = whole prompt
 
 
 @dataclass
@@ -71,6 +82,106 @@ class RoundResult:
     tokens: List[torch.Tensor]  # per microbatch: int32 [steps, Bm] (host)
     step_times_ms: List[float] = field(default_factory=list)
     prefill_ms: float = 0.0
+
+
+def prefill_chunks(lens: List[int], chunk: int) -> List[Tuple[List[int], List[int]]]:
+    """(starts, qlens) per prefill chunk for prompts of `lens` tokens.  Chunks
+    are aligned to the end of each prompt: the last chunk holds every
+    sequence's final position (its logits are sampled); earlier chunks of a
+    shorter prompt may be empty."""
+    top = max(lens)
+    if chunk <= 0 or chunk >= top:
+        return [([0] * len(lens), list(lens))]
+    C = -(-top // chunk)
+    out = []
+    for c in range(C):
+        back_hi, back_lo = (C - c - 1) * chunk, (C - c) * chunk  # distance from the end
+        starts = [max(0, n - back_lo) for n in lens]
+        ends = [max(0, n - back_hi) for n in lens]
+        out.append((starts, [e - s for s, e in zip(starts, ends)]))
+    return out
+
+
+class _Round:
+    """Buffers, metadata and comm state of one round on one stage."""
+
+    def __init__(self, w: "StageWorker", spec: RoundSpec):
+        st, dev = w.stage, w.device
+        self.w, self.spec = w, spec
+        self.M, self.G = len(spec.microbatches), spec.steps
+        if self.G < 1 or self.M < 1:
+            raise ValueError("round needs >= 1 step and >= 1 microbatch")
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.chunk_meta: List[List[BatchMeta]] = []   # [m][c]
+        self.chunk_ids: List[List[torch.Tensor]] = []  # stage 0: [m][c] prompt ids
+        self.dec_meta, self.samp = [], []
+        self.in_pre, self.in_dec, self.tok_in, self.tok_out = [], [], [], []
+        per_mb = []
+        for mb in spec.microbatches:
+            lens = [len(p) for p in mb.prompts]
+            if min(lens) < 1:
+                raise ValueError("empty prompt")
+            if max(lens) + self.G > st.max_seq:
+                raise ValueError(f"prompt+generation {max(lens) + self.G} exceeds max_seq {st.max_seq}")
+            per_mb.append((lens, prefill_chunks(lens, spec.prefill_chunk)))
+        # every microbatch runs the same number of steps: shorter prompts get
+        # leading empty chunks
+        C = max(len(ch) for _, ch in per_mb)
+        for mb, (lens, chunks) in zip(spec.microbatches, per_mb):
+            empty = ([0] * mb.size, [0] * mb.size)
+            chunks = [empty] * (C - len(chunks)) + chunks
+            self.chunk_meta.append([BatchMeta.build(mb.slots, s0, q, dev) for s0, q in chunks])
+            self.dec_meta.append(BatchMeta.decode(mb.slots, lens, dev, max_ctx=max(lens) + self.G))
+            if w.last:
+                self.samp.append(SamplingState(mb.temperature, mb.top_k, mb.greedy, mb.seeds, dev))
+            if w.first:
+                self.chunk_ids.append([torch.tensor([t for p, a, n in zip(mb.prompts, s0, q)
+                                                     for t in p[a:a + n]], **i32)
+                                       for s0, q in chunks])
+                self.tok_in.append(torch.zeros(mb.size, **i32))
+                self.tok_out.append(torch.zeros(self.G, mb.size, **i32))
+            else:
+                rows = max(sum(q) for _, q in chunks)
+                self.in_pre.append(torch.empty(max(rows, 1), w.H, dtype=torch.float32, device=dev))
+                self.in_dec.append(torch.empty(mb.size, w.H, dtype=torch.float32, device=dev))
+        self.C = C
+        self.items = [(s, m) for s in range(C + self.G - 1) for m in range(self.M)]
+        self.recv: Dict[tuple, Handle] = {}
+        self.send_pending: Dict[int, SendHandle] = {}
+        self.graphs: Dict[int, tuple] = {}
+        self.step_events: List[torch.cuda.Event] = []
+
+    def rows(self, s: int, m: int) -> int:
+        return self.chunk_meta[m][s].num_tokens if s < self.C else self.spec.microbatches[m].size
+
+    def recv_target(self, s: int, m: int) -> Optional[Tuple[str, int, torch.Tensor]]:
+        """(edge, src stage, buffer) the input of item (s, m) arrives in, or None
+        when it is local (stage 0 prefill / single-stage decode) or absent."""
+        w = self.w
+        if w.first:
+            if s < self.C or w.P == 1:
+                return None
+            return ("ret", w.P - 1, self.tok_in[m])
+        if s < self.C:
+            n = self.rows(s, m)
+            return ("fwd", w.r - 1, self.in_pre[m][:n]) if n > 0 else None
+        return ("fwd", w.r - 1, self.in_dec[m])
+
+    def post(self, i: int) -> None:
+        if i >= len(self.items):
+            return
+        s, m = self.items[i]
+        tgt = self.recv_target(s, m)
+        if tgt is not None and (s, m) not in self.recv:
+            # posted from m's lane: the comm stream then also waits for the
+            # previous reader of this buffer (microbatch m's last compute)
+            with self.w.on_lane(m):
+                self.recv[(s, m)] = self.w.t.irecv(tgt[2], tgt[1], tgt[0])
+
+
+def _same_buffer(a: Optional[tuple], b: Optional[tuple]) -> bool:
+    return (a is not None and b is not None
+            and a[2].untyped_storage().data_ptr() == b[2].untyped_storage().data_ptr())
 
 
 class StageWorker:
@@ -96,6 +207,11 @@ class StageWorker:
         self.lanes = ([torch.cuda.Stream(self.device) for _ in range(n_lanes)]
                       if self.device.type == "cuda" else [])
 
+    def on_lane(self, m: int):
+        if not self.lanes:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(self.lanes[m % len(self.lanes)])
+
     # ------------------------------------------------------------------
     def _sync(self) -> None:
         if self.stream is not None:
@@ -111,165 +227,117 @@ class StageWorker:
         return res
 
     def _run_round(self, spec: RoundSpec) -> Optional[RoundResult]:
-        st, dev, P, r = self.stage, self.device, self.P, self.r
-        mbs = spec.microbatches
-        M, G = len(mbs), spec.steps
-        if G < 1 or M < 1:
-            raise ValueError("round needs >= 1 step and >= 1 microbatch")
-        i32 = dict(dtype=torch.int32, device=dev)
-        vocab = st.cfg.vocab_size
-
-        pre_meta, dec_meta, samp = [], [], []
-        prompt_ids, in_pre, in_dec, tok_in, tok_out = [], [], [], [], []
-        for mb in mbs:
-            lens = [len(p) for p in mb.prompts]
-            if min(lens) < 1:
-                raise ValueError("empty prompt")
-            if max(lens) + G > st.max_seq:
-                raise ValueError(f"prompt+generation {max(lens) + G} exceeds max_seq {st.max_seq}")
-            pre_meta.append(BatchMeta.build(mb.slots, [0] * mb.size, lens, dev))
-            dec_meta.append(BatchMeta.decode(mb.slots, lens, dev, max_ctx=max(lens) + G))
-            if self.last:
-                samp.append(SamplingState(mb.temperature, mb.top_k, mb.greedy, mb.seeds, dev))
-            if self.first:
-                flat = [t for p in mb.prompts for t in p]
-                prompt_ids.append(torch.tensor(flat, **i32))
-                tok_in.append(torch.zeros(mb.size, **i32))
-                tok_out.append(torch.zeros(G, mb.size, **i32))
-            if not self.first:
-                in_pre.append(torch.empty(sum(lens), self.H, dtype=torch.float32, device=dev))
-                in_dec.append(torch.empty(mb.size, self.H, dtype=torch.float32, device=dev))
-
+        dev, P = self.device, self.P
+        R = _Round(self, spec)
         L = max(1, len(self.lanes))
         for lane in self.lanes:
             lane.wait_stream(torch.cuda.current_stream(dev))
         # kernels size their grids for the lanes that actually run side by side
-        st.backend.concurrency = min(L, M)
-
-        def on_lane(m):
-            if not self.lanes:
-                return contextlib.nullcontext()
-            return torch.cuda.stream(self.lanes[m % L])
-
-        items = [(s, m) for s in range(G) for m in range(M)]
-        recv: Dict[tuple, Handle] = {}
-        send_pending: Dict[int, SendHandle] = {}
-        graphs: Dict[int, tuple] = {}
-        step_events = []
-
-        def recv_key_buf(s, m):
-            """(edge, src, buffer) the input of item (s, m) arrives in, or None."""
-            if self.first:
-                if s == 0 or P == 1:
-                    return None
-                return ("ret", P - 1, tok_in[m])
-            return ("fwd", r - 1, in_pre[m] if s == 0 else in_dec[m])
-
-        def post(i):
-            if i >= len(items):
-                return
-            s, m = items[i]
-            kb = recv_key_buf(s, m)
-            if kb is not None and (s, m) not in recv:
-                # posted from m's lane: the comm stream then also waits for the
-                # previous reader of this buffer (microbatch m's last compute)
-                with on_lane(m):
-                    recv[(s, m)] = self.t.irecv(kb[2], kb[1], kb[0])
-
-        def body(s, m, inp):
-            """Compute of item (s, m); returns what goes downstream."""
-            meta = pre_meta[m] if s == 0 else dec_meta[m]
-            st.backend.lane = m % L
-            out = st.forward(meta, inp)
-            if s > 0:
-                dec_meta[m].advance()
-            if self.last:
-                tok = st.backend.sample(out, samp[m], vocab)
-                samp[m].advance()
-                return tok
-            return out
+        self.stage.backend.concurrency = min(L, R.M)
 
         t_start = time.perf_counter()
-        post(0)
-        for i, (s, m) in enumerate(items):
-            with on_lane(m), trace_range(f"stage{r}/step{s}/mb{m}"):
-                self._item(i, s, m, items, recv, send_pending, graphs, step_events, spec, post,
-                           recv_key_buf, body, prompt_ids, tok_in, tok_out, G, P, r)
+        R.post(0)
+        for i, (s, m) in enumerate(R.items):
+            with self.on_lane(m), trace_range(f"stage{self.r}/step{s}/mb{m}"):
+                self._item(R, i, s, m)
         # Stage 0 still owes the receive of the final step's tokens.
         if self.first and P > 1:
-            for m in range(M):
-                with on_lane(m):
-                    self.t.irecv(tok_in[m], P - 1, "ret").wait()
-                    tok_out[m][G - 1].copy_(tok_in[m])
-        for h in send_pending.values():
+            for m in range(R.M):
+                with self.on_lane(m):
+                    self.t.irecv(R.tok_in[m], P - 1, "ret").wait()
+                    R.tok_out[m][R.G - 1].copy_(R.tok_in[m])
+        for h in R.send_pending.values():
             h.wait()
         for lane in self.lanes:
             torch.cuda.current_stream(dev).wait_stream(lane)
-        if spec.record_timing and self.first and self.device.type == "cuda":
+        if spec.record_timing and self.first and dev.type == "cuda":
             ev = torch.cuda.Event(enable_timing=True)
-            with on_lane(0):
+            with self.on_lane(0):
                 ev.record()
-            step_events.append(ev)
+            R.step_events.append(ev)
         self._sync()
         elapsed = (time.perf_counter() - t_start) * 1e3
         if not self.first:
             return None
-        res = RoundResult(tokens=[t.cpu() for t in tok_out])
-        if step_events:
-            ts = [step_events[k].elapsed_time(step_events[k + 1]) for k in range(len(step_events) - 1)]
-            res.prefill_ms = ts[0] if ts else 0.0
-            res.step_times_ms = ts[1:]
+        res = RoundResult(tokens=[t.cpu() for t in R.tok_out])
+        ev = R.step_events
+        if ev:
+            ts = [ev[k].elapsed_time(ev[k + 1]) for k in range(len(ev) - 1)]
+            res.prefill_ms = sum(ts[:R.C])
+            res.step_times_ms = ts[R.C:]
         else:
             res.prefill_ms = elapsed
         return res
 
-    def _item(self, i, s, m, items, recv, send_pending, graphs, step_events, spec, post,
-              recv_key_buf, body, prompt_ids, tok_in, tok_out, G, P, r):
+    def _body(self, R: _Round, s: int, m: int, inp):
+        """Compute of item (s, m); returns what goes downstream (None: nothing)."""
+        st = self.stage
+        st.backend.lane = m % max(1, len(self.lanes))
+        prefill = s < R.C
+        if prefill and R.rows(s, m) == 0:  # this microbatch's prompts end before chunk s
+            return None
+        meta = R.chunk_meta[m][s] if prefill else R.dec_meta[m]
+        sample = self.last and (not prefill or s == R.C - 1)
+        out = st.forward(meta, inp, head=sample or not self.last)
+        if not prefill:
+            R.dec_meta[m].advance()
+        if sample:
+            tok = st.backend.sample(out, R.samp[m], st.cfg.vocab_size)
+            R.samp[m].advance()
+            return tok
+        return None if self.last else out
+
+    def _item(self, R: _Round, i: int, s: int, m: int) -> None:
         """One (step, microbatch) of the static schedule, on microbatch m's lane."""
-        if spec.record_timing and m == 0 and self.device.type == "cuda":
+        P = self.P
+        if R.spec.record_timing and m == 0 and self.device.type == "cuda":
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
-            step_events.append(ev)
+            R.step_events.append(ev)
         # --- input
-        if (s, m) in recv:
-            inp = recv.pop((s, m)).wait()
+        if (s, m) in R.recv:
+            inp = R.recv.pop((s, m)).wait()
         elif self.first:
-            inp = prompt_ids[m] if s == 0 else tok_in[m]
+            inp = R.chunk_ids[m][s] if s < R.C else R.tok_in[m]
+        elif R.recv_target(s, m) is None:
+            inp = None  # empty prefill chunk of this microbatch
         else:
-            raise RuntimeError(f"stage {r}: no input posted for {(s, m)}")
-        if self.first and s > 0:
-            tok_out[m][s - 1].copy_(inp)
+            raise RuntimeError(f"stage {self.r}: no input posted for {(s, m)}")
+        if self.first and s >= R.C:
+            R.tok_out[m][s - R.C].copy_(inp)
         # Post the next receive before enqueueing this compute when it
         # targets a different buffer (overlap); otherwise after.
-        cur_kb = recv_key_buf(s, m)
-        nxt_kb = recv_key_buf(*items[i + 1]) if i + 1 < len(items) else None
-        early = nxt_kb is not None and (cur_kb is None or nxt_kb[2] is not cur_kb[2])
+        cur = R.recv_target(s, m)
+        nxt = R.recv_target(*R.items[i + 1]) if i + 1 < len(R.items) else None
+        early = nxt is not None and not _same_buffer(cur, nxt)
         if early:
-            post(i + 1)
+            R.post(i + 1)
         # --- the previous send of this microbatch's static output must be done
-        if m in send_pending:
-            send_pending.pop(m).wait()
+        if m in R.send_pending:
+            R.send_pending.pop(m).wait()
         # --- compute
-        use_graph = spec.use_graphs and self.device.type == "cuda" and s >= 2
+        use_graph = R.spec.use_graphs and self.device.type == "cuda" and s >= R.C + 1
         if use_graph:
-            if m not in graphs:
-                graphs[m] = self._capture(lambda s=s, m=m, inp=inp: body(s, m, inp))
-            g, out = graphs[m]
+            if m not in R.graphs:
+                R.graphs[m] = self._capture(lambda s=s, m=m, inp=inp: self._body(R, s, m, inp))
+            g, out = R.graphs[m]
             g.replay()
         else:
-            out = body(s, m, inp)
+            out = self._body(R, s, m, inp)
         if not early:
-            post(i + 1)
+            R.post(i + 1)
         # --- output
+        if out is None:
+            return
         if self.last:
             if P == 1:
-                tok_in[m].copy_(out)
-                if s == G - 1:
-                    tok_out[m][s].copy_(out)
+                R.tok_in[m].copy_(out)
+                if s == R.C + R.G - 2:
+                    R.tok_out[m][R.G - 1].copy_(out)
             else:
-                send_pending[m] = self.t.send(out, 0, "ret")
+                R.send_pending[m] = self.t.send(out, 0, "ret")
         else:
-            send_pending[m] = self.t.send(out, r + 1, "fwd")
+            R.send_pending[m] = self.t.send(out, self.r + 1, "fwd")
 
     # ------------------------------------------------------------------
     def _capture(self, fn):

@@ -217,7 +217,8 @@ class Engine:
                 greedy=[p.greedy for p in ps],
                 seeds=[p.seed if p.seed is not None else self._rng.getrandbits(62) for p in ps]))
         g = self.cfg.use_graphs if use_graphs is None else use_graphs
-        return RoundSpec(microbatches=mbs, steps=steps, use_graphs=g, record_timing=record_timing)
+        return RoundSpec(microbatches=mbs, steps=steps, use_graphs=g, record_timing=record_timing,
+                         prefill_chunk=self.cfg.prefill_chunk)
 
     def generate_ids(self, prompts: List[List[int]], params, microbatches: Optional[int] = None,
                      record_timing: bool = False) -> List[List[int]]:

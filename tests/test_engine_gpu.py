@@ -82,3 +82,12 @@ def test_gpt2_small_shapes_smoke():
         model_id="gpt2", max_batch=8, device="cuda", max_seq_len=256))
     out = e.generate_ids([[1, 2, 3]] * 8, SamplingParams(max_new_tokens=8, seed=1))
     assert all(len(o) == 8 and all(0 <= t < 50257 for t in o) for o in out)
+
+
+@pytest.mark.parametrize("model", ["gpt2-test", "llama-test"])
+def test_chunked_prefill_gpu_matches_one_shot(model):
+    prompts = [list(range(1, 90)), [5, 6, 7], list(range(100, 160)), [9] * 33]
+    sp = SamplingParams(greedy=True, max_new_tokens=8)
+    want = _engine(model).generate_ids(prompts, sp)
+    got = _engine(model, P=2, prefill_chunk=32).generate_ids(prompts, sp, microbatches=2)
+    assert got == want

@@ -220,3 +220,39 @@ def test_unit_plan_beats_whole_layers_on_xl():
         assert sum(ch) / P / max(ch) > 0.9  # within 10 % of a perfect split
     # SPLIT_AT-style explicit layer splits map to even unit boundaries
     assert make_unit_plan(mc, 2, split_points=[20]) == [(0, 40), (40, 96)]
+
+
+# ---------------------------------------------------------------------------
+# Chunked prefill: the prompt enters the KV cache in end-aligned chunks over
+# several pipeline steps; outputs must equal the one-shot prefill.
+# ---------------------------------------------------------------------------
+def test_prefill_chunks_layout():
+    from llm_sharding_demo_amd.parallel.pipeline import prefill_chunks
+
+    ch = prefill_chunks([10, 3, 7], 4)
+    assert len(ch) == 3
+    # end-aligned: the last chunk holds every sequence's final position
+    assert ch[-1] == ([6, 0, 3], [4, 3, 4])
+    for i, n in enumerate([10, 3, 7]):
+        covered = []
+        for starts, qlens in ch:
+            covered += list(range(starts[i], starts[i] + qlens[i]))
+        assert covered == list(range(n))
+    assert prefill_chunks([5, 2], 0) == [([0, 0], [5, 2])]
+
+
+LONG = [list(range(1, 30)), [5, 6, 7], list(range(100, 117)), [9] * 11, [3]]
+
+
+@pytest.mark.parametrize("model,P,chunk,M", [("gpt2-test", 1, 4, 1), ("gpt2-test", 2, 5, 2),
+                                             ("gpt2-test", 3, 8, 3), ("llama-test", 2, 6, 2)])
+def test_chunked_prefill_matches_one_shot(model, P, chunk, M):
+    sp = SamplingParams(greedy=True, max_new_tokens=5)
+    base = Engine(EngineConfig(model_id=model, num_stages=1, max_batch=8, device="cpu"))
+    want = base.generate_ids(LONG, sp)
+    eng = Engine(EngineConfig(model_id=model, num_stages=P, max_batch=8, device="cpu",
+                              prefill_chunk=chunk))
+    assert eng.generate_ids(LONG, sp, microbatches=M) == want
+    # sampled decoding is seeded per (request, token): chunking must not change it
+    sp2 = SamplingParams(temperature=0.9, top_k=10, seed=3, max_new_tokens=4)
+    assert eng.generate_ids(LONG, sp2, microbatches=M) == base.generate_ids(LONG, sp2)
