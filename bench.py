@@ -148,7 +148,7 @@ def main() -> int:
         }
         print(json.dumps(out), flush=True)
     if N > 1:
-        eng.transport.barrier()
+        eng._close_dist()  # barrier, then tear the process groups down in order
     return 0
 
 

@@ -283,16 +283,22 @@ class LocalTransport(Transport):
         self.fabric._barrier.wait(timeout=self.fabric.timeout)
 
 
-def init_distributed(backend: str, device_type: str) -> None:
+def init_distributed(backend: str, device_type: str, timeout_s: float = 600.0) -> None:
     """Initialise torch.distributed from torchrun env vars (RANK, WORLD_SIZE,
-    LOCAL_RANK, MASTER_ADDR/PORT).  Binds the process to its GPU first."""
+    LOCAL_RANK, MASTER_ADDR/PORT).  Binds the process to its GPU first.
+
+    `timeout_s` bounds every collective / p2p op: with RCCL's async error
+    handling a peer that died or hung turns into an exception on the waiting
+    ranks after the timeout instead of a silent hang."""
+    import datetime
     import os
 
     import torch.distributed as dist
 
     if dist.is_initialized():
         return
-    kw = {}
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    kw = {"timeout": datetime.timedelta(seconds=timeout_s)}
     if device_type == "cuda":
         # one rank per GPU; more ranks than GPUs (single-GPU rehearsal over
         # gloo) wrap around.  device_count() does not initialise HIP.

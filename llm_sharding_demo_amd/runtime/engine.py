@@ -100,7 +100,7 @@ class Engine:
             dev = resolve_device(cfg.device)
             kind = cfg.transport if cfg.transport not in ("auto", "local") else (
                 "nccl" if dev.type == "cuda" else "gloo")
-            init_distributed("nccl" if kind == "nccl" else "gloo", dev.type)
+            init_distributed("nccl" if kind == "nccl" else "gloo", dev.type, cfg.round_timeout_s)
             self.rank = dist.get_rank()
             if dev.type == "cuda":
                 dev = torch.device("cuda", torch.cuda.current_device())
