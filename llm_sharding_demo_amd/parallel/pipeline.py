@@ -82,6 +82,10 @@ class RoundResult:
     tokens: List[torch.Tensor]  # per microbatch: int32 [steps, Bm] (host)
     step_times_ms: List[float] = field(default_factory=list)
     prefill_ms: float = 0.0
+    # per stage (record_timing rounds): {"stage", "wall_ms", "busy_ms",
+    # "busy_fraction", "items"} -- busy = union of this stage's compute
+    # intervals over both lanes; 1 - busy_fraction is the stage's bubble
+    stages: List[dict] = field(default_factory=list)
 
 
 def prefill_chunks(lens: List[int], chunk: int) -> List[Tuple[List[int], List[int]]]:
@@ -150,6 +154,7 @@ class _Round:
         self.send_pending: Dict[int, SendHandle] = {}
         self.graphs: Dict[int, tuple] = {}
         self.step_events: List[torch.cuda.Event] = []
+        self.compute_marks: List[tuple] = []  # (start, end) events / host times per item
 
     def rows(self, s: int, m: int) -> int:
         return self.chunk_meta[m][s].num_tokens if s < self.C else self.spec.microbatches[m].size
@@ -203,6 +208,7 @@ class StageWorker:
         # phases (small GEMMs, split-K tails) run beside another's bandwidth-
         # bound ones (attention over the KV cache).  Each lane has its own
         # split-K ticket counters in the backend.
+        self.last_stats: Optional[dict] = None  # per-stage timing of the last timed round
         n_lanes = int(os.environ.get("LSD_LANES", "2"))
         self.lanes = ([torch.cuda.Stream(self.device) for _ in range(n_lanes)]
                       if self.device.type == "cuda" else [])
@@ -236,6 +242,11 @@ class StageWorker:
         self.stage.backend.concurrency = min(L, R.M)
 
         t_start = time.perf_counter()
+        timing = spec.record_timing
+        t0_ev = None
+        if timing and dev.type == "cuda":
+            t0_ev = torch.cuda.Event(enable_timing=True)
+            t0_ev.record()
         R.post(0)
         for i, (s, m) in enumerate(R.items):
             with self.on_lane(m), trace_range(f"stage{self.r}/step{s}/mb{m}"):
@@ -255,8 +266,13 @@ class StageWorker:
             with self.on_lane(0):
                 ev.record()
             R.step_events.append(ev)
+        t1_ev = None
+        if t0_ev is not None:
+            t1_ev = torch.cuda.Event(enable_timing=True)
+            t1_ev.record()
         self._sync()
         elapsed = (time.perf_counter() - t_start) * 1e3
+        self.last_stats = self._stage_stats(R, t0_ev, t1_ev, t_start, elapsed) if timing else None
         if not self.first:
             return None
         res = RoundResult(tokens=[t.cpu() for t in R.tok_out])
@@ -267,7 +283,29 @@ class StageWorker:
             res.step_times_ms = ts[R.C:]
         else:
             res.prefill_ms = elapsed
+        if self.last_stats is not None:
+            res.stages = [self.last_stats]
         return res
+
+    def _stage_stats(self, R: _Round, t0_ev, t1_ev, t_start: float, elapsed: float) -> dict:
+        if t0_ev is not None:
+            iv = sorted((t0_ev.elapsed_time(a), t0_ev.elapsed_time(b)) for a, b in R.compute_marks)
+            wall = t0_ev.elapsed_time(t1_ev)
+        else:  # CPU: compute is synchronous, host clocks are the compute intervals
+            iv = sorted(((a - t_start) * 1e3, (b - t_start) * 1e3) for a, b in R.compute_marks)
+            wall = elapsed
+        busy, cur = 0.0, None
+        for a, b in iv:
+            if cur is None or a > cur[1]:
+                if cur is not None:
+                    busy += cur[1] - cur[0]
+                cur = [a, b]
+            else:
+                cur[1] = max(cur[1], b)
+        if cur is not None:
+            busy += cur[1] - cur[0]
+        return {"stage": self.r, "wall_ms": round(wall, 3), "busy_ms": round(busy, 3),
+                "busy_fraction": round(busy / wall, 4) if wall > 0 else 0.0, "items": len(iv)}
 
     def _body(self, R: _Round, s: int, m: int, inp):
         """Compute of item (s, m); returns what goes downstream (None: nothing)."""
@@ -317,6 +355,7 @@ class StageWorker:
             R.send_pending.pop(m).wait()
         # --- compute
         use_graph = R.spec.use_graphs and self.device.type == "cuda" and s >= R.C + 1
+        mark = self._mark() if R.spec.record_timing else None
         if use_graph:
             if m not in R.graphs:
                 R.graphs[m] = self._capture(lambda s=s, m=m, inp=inp: self._body(R, s, m, inp))
@@ -324,6 +363,8 @@ class StageWorker:
             g.replay()
         else:
             out = self._body(R, s, m, inp)
+        if mark is not None:
+            R.compute_marks.append((mark, self._mark()))
         if not early:
             R.post(i + 1)
         # --- output
@@ -338,6 +379,15 @@ class StageWorker:
                 R.send_pending[m] = self.t.send(out, 0, "ret")
         else:
             R.send_pending[m] = self.t.send(out, self.r + 1, "fwd")
+
+    def _mark(self):
+        """Timestamp on the current (lane) stream: a timing event on the GPU,
+        the host clock on CPU."""
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.perf_counter()
 
     # ------------------------------------------------------------------
     def _capture(self, fn):

@@ -140,6 +140,12 @@ class Engine:
     def _dist_round(self, specs) -> List[Optional[RoundResult]]:
         spec = specs[self.replica]
         res = self.workers[0].run_round(spec) if spec is not None else None
+        if any(sp is not None and sp.record_timing for sp in specs):
+            # per-stage busy / bubble figures of every rank, to the coordinator
+            stats = self.transport.gather_object(self.workers[0].last_stats if spec else None, dst=0)
+            if stats is not None and res is not None:
+                res.stages = [dict(st, replica=g // self.P) for g, st in enumerate(stats)
+                              if st is not None]
         if self.R == 1:
             return [res]
         # stage 0 of every replica holds its replica's tokens; collect on rank 0
@@ -169,6 +175,8 @@ class Engine:
             t.join()
         if errors:
             raise errors[0]
+        if spec.record_timing:
+            results[0].stages = [w.last_stats for w in self.workers if w.last_stats is not None]
         return results[0]
 
     def worker_loop(self) -> None:

@@ -145,7 +145,7 @@ class RequestBatcher:
                     r.t_start = t0
                 try:
                     outs = self.engine.generate_ids([r.prompt_ids for r in group],
-                                                     [r.params for r in group])
+                                                     [r.params for r in group], record_timing=True)
                     for r, o in zip(group, outs):
                         r.output = o
                 except BaseException as e:  # fail the whole group, keep serving

@@ -209,6 +209,11 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
                      "batched_rounds_total": batcher.stats["batches"],
                      "batched_requests_total": batcher.stats["requests"],
                      "max_batch_seen": batcher.stats["max_batch_seen"]}
+            lr = engine.last_round
+            for st in (lr.stages if lr is not None else []):
+                tag = f"stage{st['stage']}" + (f"_replica{st['replica']}" if st.get("replica") else "")
+                extra[f"{tag}_busy_fraction"] = st["busy_fraction"]
+                extra[f"{tag}_bubble_fraction"] = 1.0 - st["busy_fraction"]
         return metrics.render(extra)
 
     return app

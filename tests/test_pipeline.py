@@ -154,7 +154,10 @@ def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp):
             eng.worker_loop()
         else:
             out = eng.generate_ids({PROMPTS!r}, SamplingParams(greedy=True, max_new_tokens=6))
-            out2 = eng.generate_ids({PROMPTS!r}[:2], SamplingParams(greedy=True, max_new_tokens=6))
+            out2 = eng.generate_ids({PROMPTS!r}[:2], SamplingParams(greedy=True, max_new_tokens=6),
+                                    record_timing=True)
+            stages = eng.last_round.stages
+            assert sorted(st["stage"] for st in stages) == sorted(list(range(eng.P)) * {dp}), stages
             eng.shutdown()
             print("RESULT", json.dumps([out, out2]))
     """))
@@ -256,3 +259,12 @@ def test_chunked_prefill_matches_one_shot(model, P, chunk, M):
     # sampled decoding is seeded per (request, token): chunking must not change it
     sp2 = SamplingParams(temperature=0.9, top_k=10, seed=3, max_new_tokens=4)
     assert eng.generate_ids(LONG, sp2, microbatches=M) == base.generate_ids(LONG, sp2)
+
+
+def test_stage_busy_stats_local_and_gloo():
+    eng = Engine(EngineConfig(model_id="gpt2-test", num_stages=3, max_batch=8, device="cpu"))
+    eng.generate_ids(PROMPTS, SamplingParams(greedy=True, max_new_tokens=4), microbatches=3,
+                     record_timing=True)
+    st = eng.last_round.stages
+    assert [s["stage"] for s in st] == [0, 1, 2]
+    assert all(0.0 < s["busy_fraction"] <= 1.0 and s["items"] > 0 for s in st)

@@ -88,7 +88,7 @@ class _SlowEngine:
         self.slots = type("S", (), {"capacity": 4})()
         self.release = threading.Event()
 
-    def generate_ids(self, prompts, params):
+    def generate_ids(self, prompts, params, **kw):
         self.round_started = time.monotonic()
         self.release.wait(30)
         self.round_started = None
@@ -135,4 +135,5 @@ def test_http_concurrent_generate_batched():
     assert all("generated" in r and r["generated"].startswith(f"hi {i}") for i, r in enumerate(res))
     m = client.get("/metrics").text
     assert "llmshard_batched_requests_total 6" in m
+    assert "llmshard_stage1_busy_fraction" in m and "llmshard_token_latency_p50_ms" in m
     assert app.state.batcher.stats["batches"] < 6
