@@ -32,140 +32,147 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, long ldq, const bf16* __restrict__ kc,
     const bf16* __restrict__ vc, const int* __restrict__ seq_slots,
     const int* __restrict__ qpos, bf16* out, long ldo, float* part_o, float* part_ml, int n_kv,
-    int max_seq, int splits, float scale_log2) {
+    int max_seq, int splits, float scale_log2, int n_items) {
   constexpr int LPK = HD / 8;    // lanes per key row
   constexpr int KPI = 64 / LPK;  // keys per wave-instruction
-  const int b = blockIdx.x / n_kv, kvh = blockIdx.x % n_kv, split = blockIdx.y;
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int ds = lane % LPK, kg = lane / LPK;
-  const int ctx = qpos[b] + 1;
-  const int per = (ctx + splits - 1) / splits;
-  const int k_lo = split * per, k_hi = min(ctx, k_lo + per);
-  const long base = ((long)seq_slots[b] * n_kv + kvh) * (long)max_seq * HD + ds * 8;
-
-  float qf[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    bf16x8 qq = ld8(q + (long)b * ldq + (long)(kvh * G + g) * HD + ds * 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[g][j] = bf2f(qq[j]) * scale_log2;
-  }
-  float m[G], l[G], o[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    m[g] = NEG;
-    l[g] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
-  }
-
-  for (int c0 = k_lo + w * KPI; c0 < k_hi; c0 += 4 * KPI * U) {
-    bf16x8 kv[U];
-    int key[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      key[u] = c0 + u * 4 * KPI + kg;
-      const int kk = min(key[u], k_hi - 1);
-      kv[u] = ld8(kc + base + (long)kk * HD);
-    }
-    float s[G][U];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        float acc = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += qf[g][j] * bf2f(kv[u][j]);
-#pragma unroll
-        for (int msk = 1; msk < LPK; msk <<= 1) acc += shfl_xor(acc, msk);
-        s[g][u] = key[u] < k_hi ? acc : NEG;
-      }
-    bf16x8 vv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) vv[u] = ld8(vc + base + (long)min(key[u], k_hi - 1) * HD);
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float mx = s[g][0];
-#pragma unroll
-      for (int u = 1; u < U; ++u) mx = fmaxf(mx, s[g][u]);
-      const float mn = fmaxf(m[g], mx);
-      const float alpha = exp2f(m[g] - mn);
-      float p[U], ps = 0.f;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        p[u] = exp2f(s[g][u] - mn);
-        ps += p[u];
-      }
-      l[g] = l[g] * alpha + ps;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float a = o[g][j] * alpha;
-#pragma unroll
-        for (int u = 0; u < U; ++u) a += p[u] * bf2f(vv[u][j]);
-        o[g][j] = a;
-      }
-      m[g] = mn;
-    }
-  }
-
-  // merge the key groups of this wave (lanes with equal ds)
-#pragma unroll
-  for (int msk = LPK; msk < 64; msk <<= 1) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float mo = shfl_xor(m[g], msk), lo = shfl_xor(l[g], msk);
-      const float mn = fmaxf(m[g], mo);
-      const float a = exp2f(m[g] - mn), bb = exp2f(mo - mn);
-      l[g] = l[g] * a + lo * bb;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + shfl_xor(o[g][j], msk) * bb;
-      m[g] = mn;
-    }
-  }
-  // merge the 4 waves through LDS
   __shared__ float sm[4][G][LPK][10];
-  if (kg == 0) {
+  // work item = (sequence, kv head); a capped grid (lsd_attn_set_max_wg) loops
+  // over items so the kernel occupies only part of the chip and a concurrent
+  // lane's GEMMs keep the rest
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const int b = item / n_kv, kvh = item % n_kv, split = blockIdx.y;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int ds = lane % LPK, kg = lane / LPK;
+    const int ctx = qpos[b] + 1;
+    const int per = (ctx + splits - 1) / splits;
+    const int k_lo = split * per, k_hi = min(ctx, k_lo + per);
+    const long base = ((long)seq_slots[b] * n_kv + kvh) * (long)max_seq * HD + ds * 8;
+
+    float qf[G][8];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      sm[w][g][ds][0] = m[g];
-      sm[w][g][ds][1] = l[g];
+      bf16x8 qq = ld8(q + (long)b * ldq + (long)(kvh * G + g) * HD + ds * 8);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sm[w][g][ds][2 + j] = o[g][j];
+      for (int j = 0; j < 8; ++j) qf[g][j] = bf2f(qq[j]) * scale_log2;
     }
-  }
-  __syncthreads();
-  if (w != 0 || kg != 0) return;
+    float m[G], l[G], o[G][8];
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float mm = NEG;
+    for (int g = 0; g < G; ++g) {
+      m[g] = NEG;
+      l[g] = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) mm = fmaxf(mm, sm[ww][g][ds][0]);
-    float ll = 0.f, oo[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-      const float f = exp2f(sm[ww][g][ds][0] - mm);
-      ll += sm[ww][g][ds][1] * f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) oo[j] += sm[ww][g][ds][2 + j] * f;
+      for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
     }
-    const int h = kvh * G + g;
-    if (splits == 1) {
-      const float inv = ll > 0.f ? 1.f / ll : 0.f;
-      bf16x8 r;
+
+    for (int c0 = k_lo + w * KPI; c0 < k_hi; c0 += 4 * KPI * U) {
+      bf16x8 kv[U];
+      int key[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = f2bf(oo[j] * inv);
-      st8(out + (long)b * ldo + (long)h * HD + ds * 8, r);
-    } else {
-      const int nh = n_kv * G;
-      const long pi = ((long)b * nh + h) * splits + split;
-      float* po = part_o + pi * HD + ds * 8;
+      for (int u = 0; u < U; ++u) {
+        key[u] = c0 + u * 4 * KPI + kg;
+        const int kk = min(key[u], k_hi - 1);
+        kv[u] = ld8(kc + base + (long)kk * HD);
+      }
+      float s[G][U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) po[j] = oo[j];
-      if (ds == 0) {
-        part_ml[pi * 2] = mm;
-        part_ml[pi * 2 + 1] = ll;
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float acc = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc += qf[g][j] * bf2f(kv[u][j]);
+#pragma unroll
+          for (int msk = 1; msk < LPK; msk <<= 1) acc += shfl_xor(acc, msk);
+          s[g][u] = key[u] < k_hi ? acc : NEG;
+        }
+      bf16x8 vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) vv[u] = ld8(vc + base + (long)min(key[u], k_hi - 1) * HD);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float mx = s[g][0];
+#pragma unroll
+        for (int u = 1; u < U; ++u) mx = fmaxf(mx, s[g][u]);
+        const float mn = fmaxf(m[g], mx);
+        const float alpha = exp2f(m[g] - mn);
+        float p[U], ps = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          p[u] = exp2f(s[g][u] - mn);
+          ps += p[u];
+        }
+        l[g] = l[g] * alpha + ps;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float a = o[g][j] * alpha;
+#pragma unroll
+          for (int u = 0; u < U; ++u) a += p[u] * bf2f(vv[u][j]);
+          o[g][j] = a;
+        }
+        m[g] = mn;
       }
     }
+
+    // merge the key groups of this wave (lanes with equal ds)
+#pragma unroll
+    for (int msk = LPK; msk < 64; msk <<= 1) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float mo = shfl_xor(m[g], msk), lo = shfl_xor(l[g], msk);
+        const float mn = fmaxf(m[g], mo);
+        const float a = exp2f(m[g] - mn), bb = exp2f(mo - mn);
+        l[g] = l[g] * a + lo * bb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + shfl_xor(o[g][j], msk) * bb;
+        m[g] = mn;
+      }
+    }
+    // merge the 4 waves through LDS
+    if (kg == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        sm[w][g][ds][0] = m[g];
+        sm[w][g][ds][1] = l[g];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sm[w][g][ds][2 + j] = o[g][j];
+      }
+    }
+    __syncthreads();
+    if (w == 0 && kg == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float mm = NEG;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) mm = fmaxf(mm, sm[ww][g][ds][0]);
+        float ll = 0.f, oo[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+          const float f = exp2f(sm[ww][g][ds][0] - mm);
+          ll += sm[ww][g][ds][1] * f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) oo[j] += sm[ww][g][ds][2 + j] * f;
+        }
+        const int h = kvh * G + g;
+        if (splits == 1) {
+          const float inv = ll > 0.f ? 1.f / ll : 0.f;
+          bf16x8 r;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = f2bf(oo[j] * inv);
+          st8(out + (long)b * ldo + (long)h * HD + ds * 8, r);
+        } else {
+          const int nh = n_kv * G;
+          const long pi = ((long)b * nh + h) * splits + split;
+          float* po = part_o + pi * HD + ds * 8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) po[j] = oo[j];
+          if (ds == 0) {
+            part_ml[pi * 2] = mm;
+            part_ml[pi * 2 + 1] = ll;
+          }
+        }
+      }
+    }
+    __syncthreads();  // sm is reused by this block's next item
   }
 }
 
@@ -339,6 +346,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
 
 using namespace lsd;
 
+static int g_attn_max_wg = 0;  // 0: one workgroup per (sequence, kv head)
+extern "C" void lsd_attn_set_max_wg(int v) { g_attn_max_wg = v; }
+
 extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
                                       const int* seq_slots, const int* qpos, bf16* out, long ldo,
                                       float* part_o, float* part_ml, int B, int nh, int n_kv,
@@ -346,12 +356,14 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
                                       hipStream_t st) {
   if (B == 0) return hipSuccess;
   const int G = nh / n_kv;
-  dim3 grid(B * n_kv, splits), block(256);
+  const int n_items = B * n_kv;
+  const int gx = g_attn_max_wg > 0 ? (n_items < g_attn_max_wg ? n_items : g_attn_max_wg) : n_items;
+  dim3 grid(gx, splits), block(256);
 #define LSD_DEC(HDV, GV)                                                                      \
   if (hd == HDV && G == GV) {                                                                 \
     hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 4>), grid, block, 0, st, q, ldq, kc, vc,  \
                        seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq, splits,     \
-                       scale_log2);                                                           \
+                       scale_log2, n_items);                                                  \
     goto combine;                                                                             \
   }
   LSD_DEC(64, 1)

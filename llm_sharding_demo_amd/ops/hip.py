@@ -101,6 +101,7 @@ class HipBackend(Backend):
         self.C = _load()
         self.C.gemm_set_sk_rows(self.SK_ROWS)
         self.C.gemm_set_nw2_rows(self.NW2_ROWS)
+        self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.counters = None
         self._rope = None
         self.lane = 0  # microbatch lane (stream) currently being issued; see pipeline.py

@@ -224,7 +224,17 @@ def test_qkv_kv_append(C, CNT, rope, mode):
 
 @pytest.mark.parametrize("hd,nh,n_kv", [(64, 4, 4), (64, 8, 2), (128, 8, 2), (128, 32, 8)])
 @pytest.mark.parametrize("splits", [1, 3])
-def test_attention_decode(C, hd, nh, n_kv, splits):
+@pytest.mark.parametrize("max_wg", [0, 3])
+def test_attention_decode(C, hd, nh, n_kv, splits, max_wg):
+    """max_wg > 0: capped grid, each block loops over (sequence, head) items."""
+    C.attn_set_max_wg(max_wg)
+    try:
+        _attention_decode_case(C, hd, nh, n_kv, splits)
+    finally:
+        C.attn_set_max_wg(0)
+
+
+def _attention_decode_case(C, hd, nh, n_kv, splits):
     B, slots, S = 5, 6, 300
     kc, vc = bf(slots, n_kv, S, hd, seed=16), bf(slots, n_kv, S, hd, seed=17)
     q = bf(B, nh * hd, seed=18)
