@@ -27,6 +27,16 @@ namespace lsd {
 
 constexpr float NEG = -1e30f;
 
+// K/V rows of the decode step are streamed once per layer per step: load them
+// non-temporal so they do not evict the weights the other microbatch lane is
+// about to re-read from the Infinity Cache (bench A/B, tools/gpu_ab_flags.sh:
+// 31.8k -> 32.6k tok/s GPT-2 XL; -DLSD_KV_TEMPORAL restores default policy)
+#ifdef LSD_KV_TEMPORAL
+#define LSD_KV_LOAD ld8
+#else
+#define LSD_KV_LOAD ld8_nt
+#endif
+
 template <int HD, int G, int U>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16* __restrict__ q, long ldq, const bf16* __restrict__ kc,
@@ -71,7 +81,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       for (int u = 0; u < U; ++u) {
         key[u] = c0 + u * 4 * KPI + kg;
         const int kk = min(key[u], k_hi - 1);
-        kv[u] = ld8(kc + base + (long)kk * HD);
+        kv[u] = LSD_KV_LOAD(kc + base + (long)kk * HD);
       }
       float s[G][U];
 #pragma unroll
@@ -87,7 +97,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
         }
       bf16x8 vv[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) vv[u] = ld8(vc + base + (long)min(key[u], k_hi - 1) * HD);
+      for (int u = 0; u < U; ++u) vv[u] = LSD_KV_LOAD(vc + base + (long)min(key[u], k_hi - 1) * HD);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float mx = s[g][0];

@@ -32,6 +32,12 @@ __device__ __forceinline__ bf16x8 ld8(const bf16* p) {
   u32x4 v = *reinterpret_cast<const u32x4*>(p);
   return __builtin_bit_cast(bf16x8, v);
 }
+// Streaming (non-temporal) 16-byte load: data read once per step (KV cache)
+// need not displace reusable lines (weights re-read by the next microbatch).
+__device__ __forceinline__ bf16x8 ld8_nt(const bf16* p) {
+  u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return __builtin_bit_cast(bf16x8, v);
+}
 __device__ __forceinline__ void st8(bf16* p, bf16x8 v) {
   *reinterpret_cast<u32x4*>(p) = __builtin_bit_cast(u32x4, v);
 }
