@@ -42,7 +42,10 @@ __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids,
 }
 
 // Row kernel: H <= 4 * 256 * MAXV floats kept in registers between passes.
-template <int MAXV, bool RMS>
+// SPL >= 0: exactly SPL split-K slabs, every slab load of the row issued
+// before the first add (one memory round trip instead of one per slab: the
+// runtime-count loop serialised them, ~1 us each); SPL < 0: runtime count.
+template <int MAXV, bool RMS, int SPL>
 __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __restrict__ slab,
                                                    int splits, const bf16* __restrict__ pbias,
                                                    const bf16* __restrict__ w,
@@ -65,24 +68,47 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __rest
   float* xr = x + (long)src * H;
   f32x4 v[MAXV];
   float s1 = 0.f;
+  // GRP column groups of the row are loaded per round trip (all of them
+  // unless the slab count would blow the register budget)
+  constexpr int NL = SPL > 0 ? SPL : 0;
+  constexpr int GRP = MAXV * (NL + 1) <= 24 ? MAXV : 1;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = (threadIdx.x + i * 256) * 4;
-    if (c < H) {
-      f32x4 a = *reinterpret_cast<const f32x4*>(xr + c);
-      if (slab) {
-        for (int s = 0; s < splits; ++s)
-          a += *reinterpret_cast<const f32x4*>(slab + ((long)s * T + src) * H + c);
-        if (pbias) {
-          bf16x4 pb = ld4(pbias + c);
-          a += f32x4{bf2f(pb[0]), bf2f(pb[1]), bf2f(pb[2]), bf2f(pb[3])};
+  for (int i0 = 0; i0 < MAXV; i0 += GRP) {
+    f32x4 xa[GRP], part[GRP][NL > 0 ? NL : 1];
+    bf16x4 pbv[GRP];
+#pragma unroll
+    for (int g = 0; g < GRP; ++g) {
+      const int cc = min((threadIdx.x + (i0 + g) * 256) * 4, H - 4);  // clamped: always valid
+      xa[g] = *reinterpret_cast<const f32x4*>(xr + cc);
+      if (slab && pbias) pbv[g] = ld4(pbias + cc);
+#pragma unroll
+      for (int s = 0; s < NL; ++s)
+        part[g][s] = __builtin_nontemporal_load(
+            reinterpret_cast<const f32x4*>(slab + ((long)s * T + src) * H + cc));
+    }
+#pragma unroll
+    for (int g = 0; g < GRP; ++g) {
+      const int i = i0 + g;
+      const int c = (threadIdx.x + i * 256) * 4;
+      if (c < H) {
+        f32x4 a = xa[g];
+#pragma unroll
+        for (int s = 0; s < NL; ++s) a += part[g][s];
+        if (SPL < 0 && slab)
+          for (int s = 0; s < splits; ++s)
+            a += *reinterpret_cast<const f32x4*>(slab + ((long)s * T + src) * H + c);
+        if (slab) {
+          if (pbias) {
+            const bf16x4 pb = pbv[g];
+            a += f32x4{bf2f(pb[0]), bf2f(pb[1]), bf2f(pb[2]), bf2f(pb[3])};
+          }
+          *reinterpret_cast<f32x4*>(xr + c) = a;
         }
-        *reinterpret_cast<f32x4*>(xr + c) = a;
+        v[i] = a;
+        if (!RMS) s1 += a[0] + a[1] + a[2] + a[3];
+      } else {
+        v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      v[i] = a;
-      if (!RMS) s1 += a[0] + a[1] + a[2] + a[3];
-    } else {
-      v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
   if (out == nullptr) return;  // combine-only (flush)
@@ -133,13 +159,26 @@ extern "C" hipError_t lsd_norm(float* x, const float* slab, int splits, const bf
   const int n = rows ? nrows : T;
   if (n == 0) return hipSuccess;
   const int maxv = (H + 1023) / 1024;
-#define LSD_NORM(MV)                                                                          \
+#define LSD_NORM_S(MV, S)                                                                     \
   if (rms)                                                                                    \
-    hipLaunchKernelGGL((norm_kernel<MV, true>), dim3(n), dim3(256), 0, st, x, slab, splits,  \
+    hipLaunchKernelGGL((norm_kernel<MV, true, S>), dim3(n), dim3(256), 0, st, x, slab, splits, \
                        pbias, w, b, out, T, H, eps, rows);                                    \
   else                                                                                        \
-    hipLaunchKernelGGL((norm_kernel<MV, false>), dim3(n), dim3(256), 0, st, x, slab, splits, \
-                       pbias, w, b, out, T, H, eps, rows);
+    hipLaunchKernelGGL((norm_kernel<MV, false, S>), dim3(n), dim3(256), 0, st, x, slab,      \
+                       splits, pbias, w, b, out, T, H, eps, rows);
+#define LSD_NORM(MV)                   \
+  switch (slab ? splits : 0) {         \
+    case 0: LSD_NORM_S(MV, 0) break;   \
+    case 1: LSD_NORM_S(MV, 1) break;   \
+    case 2: LSD_NORM_S(MV, 2) break;   \
+    case 3: LSD_NORM_S(MV, 3) break;   \
+    case 4: LSD_NORM_S(MV, 4) break;   \
+    case 5: LSD_NORM_S(MV, 5) break;   \
+    case 6: LSD_NORM_S(MV, 6) break;   \
+    case 7: LSD_NORM_S(MV, 7) break;   \
+    case 8: LSD_NORM_S(MV, 8) break;   \
+    default: LSD_NORM_S(MV, -1) break; \
+  }
   if (maxv <= 2) {
     LSD_NORM(2)
   } else if (maxv <= 4) {
@@ -149,6 +188,7 @@ extern "C" hipError_t lsd_norm(float* x, const float* slab, int splits, const bf
   } else {
     return hipErrorInvalidValue;
   }
+#undef LSD_NORM_S
 #undef LSD_NORM
   return hipGetLastError();
 }

@@ -38,10 +38,11 @@ def test_embed(C):
     close(C.embed(ids, pos, wte, None), ref.embed(ids, pos, wte, None), 1e-6)
 
 
-@pytest.mark.parametrize("H", [128, 768, 1600, 4096])
+@pytest.mark.parametrize("H", [128, 768, 1600, 4096, 8192])
 @pytest.mark.parametrize("rms", [False, True])
-def test_norm_with_slab_combine(C, H, rms):
-    T, S = 19, 3
+@pytest.mark.parametrize("S", [1, 3, 8, 12])  # exact-count unrolled slabs (<= 8) and runtime loop
+def test_norm_with_slab_combine(C, H, rms, S):
+    T = 19
     x = torch.randn(T, H, device=DEV)
     slab = torch.randn(S, T, H, device=DEV) * 0.1
     pb = bf(H, scale=0.1, seed=3)
