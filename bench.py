@@ -38,12 +38,12 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--model", default="gpt2-xl")
-    p.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "256")),
+    p.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "512")),
                    help="sequences per GPU")
     p.add_argument("--prompt", type=int, default=128)
     p.add_argument("--gen", type=int, default=128)
     p.add_argument("--microbatches", type=int, default=int(os.environ.get("BENCH_MB", "0")),
-                   help="0 -> 2N: two 128-sequence microbatches in flight per stage")
+                   help="0 -> 2N: two microbatches (of --batch / 2 sequences) in flight per stage")
     p.add_argument("--dp", type=int, default=int(os.environ.get("BENCH_DP", "1")),
                    help="pipeline replicas: N GPUs = (N/dp)-stage pipeline x dp (default 1: ppN)")
     p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),

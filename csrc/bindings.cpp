@@ -98,7 +98,7 @@ GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, bool tile
   if (tiled) {
     TORCH_CHECK(p.K % 64 == 0, "tiled GEMM needs K % 64 == 0, got ", p.K);
   } else {
-    TORCH_CHECK(p.M >= 1 && p.M <= 128, "decode GEMM needs 1 <= M <= 128, got ", p.M);
+    TORCH_CHECK(p.M >= 1 && p.M <= 256, "decode GEMM needs 1 <= M <= 256, got ", p.M);
     TORCH_CHECK(p.K % 32 == 0, "decode GEMM needs K % 32 == 0, got ", p.K);
     TORCH_CHECK(p.N % 64 == 0, "decode GEMM needs N % 64 == 0 (pad the weight), got ", p.N);
   }

@@ -831,9 +831,13 @@ static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
 // 14.1 -> 12.1 us; well-filled grids gain nothing, lm_head loses).
 static int g_sk_rows = 64;
 static int g_rb_fill = 192;
+// At most 128 rows (MT = 8) per row block: M up to 256 always runs as >= 2
+// row blocks.
 static int sk_rblocks(int M, int N, int S) {
-  if (M <= g_sk_rows || (N / 64) * S >= g_rb_fill) return 1;
-  return (M + g_sk_rows - 1) / g_sk_rows;
+  const int need = (M + 127) / 128;
+  if (M <= g_sk_rows || (N / 64) * S >= g_rb_fill) return need;
+  const int rb = (M + g_sk_rows - 1) / g_sk_rows;
+  return rb > need ? rb : need;
 }
 // Row tiles (16 rows each) of one row block: MT is instantiated for
 // {1, 2, 3, 4, 6, 8}.  The split-K workspace is sized from this

@@ -123,6 +123,32 @@ def test_decode_gemm_wide_partial_tiles(C, CNT, M):
         C.gemm_set_nw2_rows(1 << 30)
 
 
+@pytest.mark.parametrize("M", [129, 200, 256])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_decode_gemm_two_row_blocks(C, CNT, M, splits):
+    """Decode GEMM above 128 rows runs as >= 2 row blocks of <= 128 (grid z)
+    sharing each W tile: plain / GELU / SiLU-mul / fp32 / residual epilogues."""
+    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
+
+    N, K = 384, 640
+    a, w, bias = bf(M, K, seed=50), bf(N, K, scale=0.05, seed=51), bf(N, scale=0.1, seed=52)
+    assert C.gemm_sk_rblocks(M, N, splits) >= 2
+    close(C.linear(a, w, bias, 0, False, splits, CNT), ref.linear(a, w, bias), 3e-2)
+    close(C.linear(a, w, bias, 1, False, splits, CNT), ref.gelu_new(ref.linear(a, w, bias)), 3e-2)
+    close(C.linear_f32(a, w, False, splits, CNT), ref.linear(a, w), 2e-3, 1e-3)
+    w2 = w[:256].contiguous()
+    y = C.linear(a, interleave_gate_up(w2, 128).contiguous(), None, 2, False, splits, CNT)
+    close(y, ref.silu_mul(*ref.linear(a, w2).split(128, 1)), 3e-2)
+    for defer in (False, True):
+        x = torch.randn(M, N, device=DEV)
+        x_ref = x + ref.linear(a, w, bias)
+        slab = C.linear_residual(a, w, bias, x, splits, False, CNT, defer)
+        if slab is not None:
+            C.norm(x, slab, bias, None, None, 0.0, True, None, False)
+        close(x, x_ref, 2e-3, 1e-3)
+    assert int(CNT.abs().sum()) == 0
+
+
 def test_split_k_deterministic(C, CNT):
     a, w = bf(64, 1600, seed=30), bf(4800, 1600, scale=0.03, seed=31)
     y1 = C.linear(a, w, None, 0, False, 7, CNT)
