@@ -16,8 +16,14 @@
 //                        freedom) and returns the makespan / bubble fraction
 //                        for given stage and link costs.
 //   * percentile      -- latency statistics for /metrics and bench.
+//   * BatchQueue      -- the serving scheduler's request queue (batch_queue.h):
+//                        thread-safe push from HTTP threads, window/length-group
+//                        round formation for the one scheduler thread (GIL
+//                        released while it waits).
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+
+#include "batch_queue.h"
 
 #include <algorithm>
 #include <cmath>
@@ -162,4 +168,18 @@ PYBIND11_MODULE(_runtime, m) {
   m.def("simulate_pipeline", &simulate_pipeline, py::arg("P"), py::arg("M"), py::arg("G"),
         py::arg("stage_cost"), py::arg("link") = 0.0);
   m.def("percentile", &percentile);
+  using lsd_rt::BatchQueue;
+  py::class_<BatchQueue>(m, "BatchQueue")
+      .def(py::init<int, double>(), py::arg("max_batch"), py::arg("length_ratio") = 4.0)
+      .def("push", &BatchQueue::push, py::arg("id"), py::arg("max_new_tokens"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("next_groups", &BatchQueue::next_groups, py::arg("window_s"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("close", &BatchQueue::close, py::call_guard<py::gil_scoped_release>())
+      .def("drain", &BatchQueue::drain)
+      .def_property_readonly("depth", &BatchQueue::depth)
+      .def_property_readonly("closed", &BatchQueue::closed)
+      .def_property_readonly("max_seen", &BatchQueue::max_seen)
+      .def_property_readonly("pushed", &BatchQueue::pushed)
+      .def_property_readonly("popped", &BatchQueue::popped);
 }

@@ -15,6 +15,7 @@ import sysconfig
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(ROOT, "csrc", "runtime", "runtime.cpp")
+HDR = os.path.join(ROOT, "csrc", "runtime", "batch_queue.h")
 
 
 def build(force: bool = False) -> str:
@@ -25,8 +26,11 @@ def build(force: bool = False) -> str:
     os.makedirs(os.path.dirname(stamp), exist_ok=True)
     flags = ["-O2", "-std=c++17", "-fPIC", "-shared", f"-I{pybind11.get_include()}",
              f"-I{sysconfig.get_paths()['include']}"]
-    with open(SRC, "rb") as f:
-        sig = hashlib.sha1(f.read() + " ".join(flags).encode()).hexdigest()
+    h = hashlib.sha1(" ".join(flags).encode())
+    for src in (SRC, HDR):
+        with open(src, "rb") as f:
+            h.update(f.read())
+    sig = h.hexdigest()
     if not force and os.path.exists(so) and os.path.exists(stamp) and open(stamp).read() == sig:
         return so
     tmp = so + ".tmp"

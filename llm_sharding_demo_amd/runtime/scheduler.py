@@ -8,7 +8,8 @@ concurrent requests -> 0.83 tok/s aggregate vs 0.69 for one).
 
 Here concurrent requests are coalesced into pipeline rounds:
 
-* `RequestBatcher` -- one scheduler thread owns the engine.  Callers enqueue a
+* `RequestBatcher` -- one scheduler thread owns the engine; round formation
+  runs in the native `BatchQueue` (csrc/runtime/batch_queue.h, TSan-tested).  Callers enqueue a
   request and block on its completion; the scheduler takes the first waiting
   request, keeps collecting for up to `window_ms` (or until the engine's
   batch capacity is reached), then runs ONE round for the whole group: every
@@ -23,12 +24,13 @@ Here concurrent requests are coalesced into pipeline rounds:
 """
 from __future__ import annotations
 
+import collections
+import itertools
 import logging
-import queue
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 from ..config import SamplingParams
 
@@ -62,32 +64,130 @@ class Request:
         return self._done.is_set()
 
 
+class PyBatchQueue:
+    """Pure-Python twin of the native `BatchQueue` (csrc/runtime/batch_queue.h):
+    same interface and grouping rule; the reference the tests compare the
+    native queue against, and the fallback when _runtime.so is absent."""
+
+    def __init__(self, max_batch: int, length_ratio: float = 4.0):
+        if max_batch < 1 or length_ratio < 1.0:
+            raise ValueError("max_batch >= 1 and length_ratio >= 1 required")
+        self.max_batch, self.ratio = max_batch, length_ratio
+        self._cv = threading.Condition()
+        self._q: "collections.deque" = collections.deque()
+        self._closed = False
+        self.max_seen = 0
+        self.pushed = self.popped = 0
+
+    def push(self, id: int, max_new_tokens: int) -> bool:
+        with self._cv:
+            if self._closed:
+                return False
+            self._q.append((id, max(1, max_new_tokens)))
+            self.pushed += 1
+            self._cv.notify()
+            return True
+
+    def next_groups(self, window_s: float) -> List[List[int]]:
+        with self._cv:
+            self._cv.wait_for(lambda: self._closed or self._q)
+            if self._closed:
+                return []
+            deadline = time.monotonic() + max(window_s, 0.0)
+            batch = []
+            while True:
+                while self._q and len(batch) < self.max_batch:
+                    batch.append(self._q.popleft())
+                if len(batch) >= self.max_batch or self._closed:
+                    break
+                left = deadline - time.monotonic()
+                if left <= 0 or not self._cv.wait_for(lambda: self._closed or self._q, left):
+                    break
+            self.popped += len(batch)
+            self.max_seen = max(self.max_seen, len(batch))
+        batch.sort(key=lambda it: it[1])
+        groups: List[List[int]] = []
+        first = 0
+        for id_, n in batch:
+            if not groups or n > self.ratio * first:
+                groups.append([])
+                first = n
+            groups[-1].append(id_)
+        return groups
+
+    def close(self) -> None:
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
+
+    def drain(self) -> List[int]:
+        with self._cv:
+            out = [i for i, _ in self._q]
+            self._q.clear()
+            return out
+
+    @property
+    def depth(self) -> int:
+        with self._cv:
+            return len(self._q)
+
+    @property
+    def closed(self) -> bool:
+        return self._closed
+
+
+def make_batch_queue(max_batch: int, length_ratio: float = 4.0, native: bool = True):
+    """The native queue (GIL released while the scheduler waits) when
+    _runtime.so is built, else the Python twin."""
+    if native:
+        from .native import load
+
+        R = load()
+        if R is not None and hasattr(R, "BatchQueue"):
+            return R.BatchQueue(max_batch, length_ratio)
+    return PyBatchQueue(max_batch, length_ratio)
+
+
 class RequestBatcher:
-    """Coalesce concurrent generate requests into pipeline rounds."""
+    """Coalesce concurrent generate requests into pipeline rounds.  Round
+    formation (window, capacity, length groups) lives in the batch queue
+    (native BatchQueue); this class owns the request payloads by id."""
 
     def __init__(self, engine, window_ms: float = 2.0, max_batch: Optional[int] = None,
-                 length_ratio: float = 4.0):
+                 length_ratio: float = 4.0, native: bool = True):
         self.engine = engine
         self.window = window_ms / 1e3
         # whole capacity of the engine: KV slots x pipeline replicas
         cap = engine.slots.capacity * max(1, getattr(engine, "R", 1))
         self.max_batch = min(max_batch or cap, cap)
         self.length_ratio = length_ratio
-        self._q: "queue.Queue[Optional[Request]]" = queue.Queue()
-        self._stop = threading.Event()
+        self._nq = make_batch_queue(self.max_batch, length_ratio, native)
+        self._reqs: Dict[int, Request] = {}
+        self._lock = threading.Lock()
+        self._ids = itertools.count()
         self.stats = {"batches": 0, "requests": 0, "max_batch_seen": 0}
         self._thread = threading.Thread(target=self._loop, name="lsd-batcher", daemon=True)
         self._thread.start()
 
+    @property
+    def native(self) -> bool:
+        return not isinstance(self._nq, PyBatchQueue)
+
     # ------------------------------------------------------------------
     def submit(self, prompt_ids: List[int], params: SamplingParams) -> Request:
-        if self._stop.is_set():
+        if self._nq.closed:
             raise RuntimeError("batcher is closed")
         if not self.engine.healthy:  # fail fast: the scheduler may be stuck in a dead round
             raise RuntimeError(f"engine unhealthy: {self.engine.last_error}")
         params.validate()
         req = Request(list(prompt_ids), params)
-        self._q.put(req)
+        rid = next(self._ids)
+        with self._lock:
+            self._reqs[rid] = req
+        if not self._nq.push(rid, params.max_new_tokens):
+            with self._lock:
+                self._reqs.pop(rid, None)
+            raise RuntimeError("batcher is closed")
         return req
 
     def generate(self, prompt_ids: List[int], params: SamplingParams,
@@ -96,50 +196,26 @@ class RequestBatcher:
 
     @property
     def queue_depth(self) -> int:
-        return self._q.qsize()
+        return self._nq.depth
 
     def close(self) -> None:
-        self._stop.set()
-        self._q.put(None)
+        self._nq.close()
         self._thread.join(timeout=5)
 
     # ------------------------------------------------------------------
-    def _collect(self, first: Request) -> List[Request]:
-        batch = [first]
-        deadline = time.monotonic() + self.window
-        while len(batch) < self.max_batch:
-            left = deadline - time.monotonic()
-            try:
-                r = self._q.get(timeout=max(left, 0.0)) if left > 0 else self._q.get_nowait()
-            except queue.Empty:
-                break
-            if r is None:
-                self._stop.set()
-                break
-            batch.append(r)
-        return batch
-
-    def _groups(self, batch: List[Request]) -> List[List[Request]]:
-        """Split by generation length so short requests do not ride out a long
-        round (a round runs max(max_new_tokens) steps for every sequence)."""
-        batch = sorted(batch, key=lambda r: r.params.max_new_tokens)
-        groups: List[List[Request]] = []
-        for r in batch:
-            n = max(1, r.params.max_new_tokens)
-            if groups and n <= self.length_ratio * max(1, groups[-1][0].params.max_new_tokens):
-                groups[-1].append(r)
-            else:
-                groups.append([r])
-        return groups
+    def _take(self, ids: List[int]) -> List[Request]:
+        with self._lock:
+            return [self._reqs.pop(i) for i in ids]
 
     def _loop(self) -> None:
-        while not self._stop.is_set():
-            first = self._q.get()
-            if first is None:
-                break
-            batch = self._collect(first)
-            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(batch))
-            for group in self._groups(batch):
+        while True:
+            groups = self._nq.next_groups(self.window)  # blocks (GIL released when native)
+            if not groups:
+                break  # closed
+            n = sum(len(g) for g in groups)
+            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], n)
+            for ids in groups:
+                group = self._take(ids)
                 t0 = time.monotonic()
                 for r in group:
                     r.t_start = t0
@@ -159,14 +235,9 @@ class RequestBatcher:
                 self.stats["batches"] += 1
                 self.stats["requests"] += len(group)
         # fail whatever is still queued
-        while True:
-            try:
-                r = self._q.get_nowait()
-            except queue.Empty:
-                break
-            if r is not None:
-                r.error = RuntimeError("batcher closed")
-                r._done.set()
+        for r in self._take(self._nq.drain()):
+            r.error = RuntimeError("batcher closed")
+            r._done.set()
 
 
 class Watchdog:

@@ -1,0 +1,75 @@
+"""Serving scheduler queue (csrc/runtime/batch_queue.h): the native queue
+matches its Python twin, close() wakes a waiting consumer, and a
+multi-producer stress binary runs clean under ThreadSanitizer and under
+AddressSanitizer + UBSan (host code only)."""
+import os
+import random
+import shutil
+import subprocess
+import threading
+import time
+
+import pytest
+
+from llm_sharding_demo_amd.runtime import native
+from llm_sharding_demo_amd.runtime.scheduler import PyBatchQueue
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def R():
+    native.build()
+    mod = native.load()
+    assert mod is not None
+    return mod
+
+
+def test_native_matches_python_twin(R):
+    rnd = random.Random(7)
+    items = [(i, rnd.choice([1, 2, 5, 8, 30, 100, 400])) for i in range(90)]
+    nq, pq = R.BatchQueue(32, 4.0), PyBatchQueue(32, 4.0)
+    for q in (nq, pq):
+        for i, n in items:
+            assert q.push(i, n)
+    for _ in range(3):  # 90 queued -> rounds of 32, 32, 26
+        assert nq.next_groups(0.0) == pq.next_groups(0.0)
+    assert nq.depth == pq.depth == 0
+    for q in (nq, pq):
+        q.push(1000, 3)
+        q.close()
+        assert not q.push(1001, 3)
+        assert q.next_groups(0.0) == []
+        assert q.drain() == [1000]
+
+
+def test_close_wakes_waiting_consumer(R):
+    q = R.BatchQueue(4, 4.0)
+    out = []
+    t = threading.Thread(target=lambda: out.append(q.next_groups(10.0)))
+    t.start()
+    time.sleep(0.05)
+    q.close()
+    t.join(timeout=5)
+    assert not t.is_alive() and out == [[]]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+@pytest.mark.parametrize("san", ["thread", "address,undefined"])
+def test_stress_under_sanitizers(tmp_path, san):
+    """8 producers + 1 round-forming consumer + a concurrent close.  No
+    sanitizer reports, every
+    accepted id delivered exactly once, rounds within max_batch."""
+    exe = tmp_path / "bq"
+    r = subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-pthread", f"-fsanitize={san}",
+                        "-fno-omit-frame-pointer",
+                        os.path.join(ROOT, "csrc", "runtime", "tests", "batch_queue_stress.cpp"),
+                        "-o", str(exe)], capture_output=True, text=True)
+    if r.returncode != 0 and "cannot find" in r.stderr:
+        pytest.skip(f"sanitizer runtime not available: {r.stderr[-200:]}")
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([str(exe), "8", "3000"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "ThreadSanitizer" not in r.stderr and "ERROR" not in r.stderr
+    assert r.stdout.startswith("ok ")
