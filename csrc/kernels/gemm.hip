@@ -651,6 +651,13 @@ constexpr int GSMEM = GSLOTS * GSLOT_BYTES;        // 128 KiB (== 256 x 128 fp32
 // s_waitcnt simm16 (gfx9 layout): vmcnt[3:0]+[15:14]=63, expcnt[6:4]=7, lgkmcnt[11:8]=0
 constexpr int LGKM0 = 0xC07F;
 
+// A/B knob (guide §5.5 T5): s_setprio(1) around the MFMA clusters
+#ifdef LSD_BIG_PRIO
+#define LSD_PRIO(v) __builtin_amdgcn_s_setprio(v)
+#else
+#define LSD_PRIO(v) ((void)0)
+#endif
+
 __device__ __forceinline__ int big_swz(int q) { return (0x78 >> (2 * q)) & 3; }
 
 __device__ __forceinline__ void stage_big(char* lds, const bf16* src, long ld, int row0, int row_max,
@@ -730,18 +737,22 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m
     // sched_barrier(0): keep the phase order as written -- hipcc otherwise
     // hoists every read above the MFMAs and spills the accumulators
     __builtin_amdgcn_sched_barrier(0);
+    LSD_PRIO(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(ac[i], wcur[j], acc[i][j]);
+    LSD_PRIO(0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 4; i < 8; ++i) an[i] = frag_a(s + 1, i);
     __builtin_amdgcn_sched_barrier(0);
+    LSD_PRIO(1);
 #pragma unroll
     for (int i = 4; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(ac[i], wcur[j], acc[i][j]);
+    LSD_PRIO(0);
     __builtin_amdgcn_sched_barrier(0);
     // Retire the next set's reads (long done under the 32 MFMAs) with a real
     // S_WAITCNT the waitcnt pass understands: the loop header then carries no
