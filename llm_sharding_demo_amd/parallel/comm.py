@@ -147,22 +147,37 @@ class _DistTransport(Transport):
     def barrier(self) -> None:
         self.dist.barrier(group=self.ctrl)
 
-
-class NcclTransport(_DistTransport):
-    """RCCL point-to-point over xGMI (backend 'nccl' IS RCCL on ROCm)."""
-
-    def _backend(self) -> str:
-        return "nccl"
-
     def warmup(self, device) -> None:
         """Eagerly create every edge communicator in a fixed global order so no
-        rank blocks in a lazy ncclCommInitRank while its peer waits elsewhere."""
-        dev = torch.device(device)
+        rank blocks in a lazy ncclCommInitRank while its peer waits elsewhere.
+
+        A single isend/irecv does NOT run on a group's collective communicator:
+        ProcessGroupNCCL keys it by the peer pair and creates that
+        communicator lazily (a blocking init) on the first p2p op.  In the
+        pipeline, stage 0 posts its return-edge irecv ahead of its first
+        forward send, so a lazy init there would wait for stage P-1 while
+        stage P-1 waits for the forward hop: deadlock.  So every edge does one
+        blocking p2p exchange here, in the order fwd0, fwd1, ..., ret (the same
+        on every rank): rank k joins fwd(k-1) then fwd(k), a chain that
+        completes left to right and ends with the return edge."""
+        dev = torch.device(device) if self._backend() == "nccl" else torch.device("cpu")
+        sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
         for name, g in self.groups.items():
-            if self.grank in self._members(name):
-                t = torch.ones(1, device=dev)
-                self.dist.all_reduce(t, group=g)
-        torch.cuda.synchronize(dev)
+            members = self._members(name)
+            if self.grank not in members:
+                continue
+            t = torch.ones(1, device=dev)
+            self.dist.all_reduce(t, group=g)  # the group's collective communicator
+            src, dst = members  # fwd: lower stage -> higher; ret: P-1 -> 0
+            buf = torch.full((1,), float(src), device=dev)
+            if self.grank == src:
+                self.dist.isend(buf, dst, group=g).wait()
+            else:
+                self.dist.irecv(buf, src, group=g).wait()
+                sync()
+                if float(buf.item()) != float(src):
+                    raise TransportError(f"warmup p2p on {name}: got {buf.item()}, want {src}")
+        sync()
         self.barrier()
 
     def _members(self, name: str) -> List[int]:
@@ -173,6 +188,13 @@ class NcclTransport(_DistTransport):
             return [base + self.P - 1, base]
         i = int(kind)
         return [base + i, base + i + 1]
+
+
+class NcclTransport(_DistTransport):
+    """RCCL point-to-point over xGMI (backend 'nccl' IS RCCL on ROCm)."""
+
+    def _backend(self) -> str:
+        return "nccl"
 
     def send(self, t, dst, edge):
         g = self._edge_group(edge, self.rank, dst)
@@ -316,6 +338,6 @@ def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1) -
         return t
     if kind == "gloo":
         t = GlooTransport(num_stages, replicas)
-        t.barrier()
+        t.warmup(device)  # same edge-by-edge bring-up as RCCL (host tensors)
         return t
     raise ValueError(f"unknown transport {kind!r}")
