@@ -110,11 +110,13 @@ def main() -> int:
     barrier()
     sync()
     t0 = time.perf_counter()
-    step_ms = []
+    step_ms, prefill_ms, max_step = [], [], []
     for _ in range(args.steps):
         res = worker.run_round(spec)
         if rank == 0 and res is not None:
             step_ms += res.step_times_ms
+            prefill_ms.append(res.prefill_ms)
+            max_step.append(max(res.step_times_ms, default=0.0))
     sync()
     barrier()
     sync()
@@ -140,6 +142,10 @@ def main() -> int:
             "dtype": "bf16" if args.device != "cpu" else "fp32",
             "data": "synthetic prompts, random-init weights",
             "p50_token_latency_ms": round(p50, 4) if p50 is not None else None,
+            # stage-0 clock, mean per timed step: prefill (TTFT of the batch)
+            # and the slowest decode step (hipGraph capture happens in one)
+            "prefill_ms": round(statistics.mean(prefill_ms), 3) if prefill_ms else None,
+            "max_decode_step_ms": round(statistics.mean(max_step), 3) if max_step else None,
             "config": {"model": args.model, "global_batch": B, "seq_len": args.prompt + args.gen,
                        "prompt_len": args.prompt, "gen_tokens": args.gen, "microbatches": M,
                        "parallelism": f"pp{P}" + (f"xdp{R}" if R > 1 else ""),
