@@ -98,6 +98,13 @@ class HipBackend(Backend):
     SK_ROWS = int(os.environ.get("LSD_SK_ROWS", "64"))
     # decode GEMM 128-column tiles above this many rows (off: slower, see gemm.hip)
     NW2_ROWS = int(os.environ.get("LSD_NW2_ROWS", str(1 << 30)))
+    # above 128 rows, GEMMs at least this wide go to the 128x128 tiled kernel
+    # (4 waves of 64x64 wave tiles, 100 workgroups for GPT-2 XL's MLP-up at 256
+    # rows) while narrower ones stay on split-K.  GPT-2 XL 2 x 256 (bench
+    # default), tok/s: all split-K 41.2-41.6k, MLP-up tiled (6400) 42.1-42.3k,
+    # + QKV tiled (4800) 40.7k, everything tiled (1600) 40.1k
+    # (profiles/r1_ab_tiled_min_n.log)
+    TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "6400"))
 
     def __init__(self):
         self.C = _load()
@@ -147,11 +154,11 @@ class HipBackend(Backend):
 
     # ------------------------------------------------------------------
     @classmethod
-    def _tiled(cls, M: int) -> bool:
-        return M > cls.SK_MAX_M
+    def _tiled(cls, M: int, N: int = 0) -> bool:
+        return M > cls.SK_MAX_M or (M > 128 and N >= cls.TILED_MIN_N)
 
     def _resid_splits(self, M: int, N: int, K: int) -> int:
-        if self._tiled(M):
+        if self._tiled(M, N):
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
             return max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
         if self.DEFER_RESID:
@@ -168,7 +175,7 @@ class HipBackend(Backend):
         return max(1, min(math.ceil(target / tiles), K // 32 // self.SK_MIN_STEPS or 1))
 
     def _gemm_kw(self, M: int, N: int, K: int, nw: int = 1):
-        if self._tiled(M):
+        if self._tiled(M, N):
             return True, 1
         return False, self._sk_splits(M, N, K, nw)
 
@@ -234,7 +241,7 @@ class HipBackend(Backend):
         M, K = a.shape
         N = w.shape[0]
         splits = self._resid_splits(M, N, K)
-        tiled = self._tiled(M)
+        tiled = self._tiled(M, N)
         # decode split-K: hand the S partial slabs to the next norm (which
         # reads the rows anyway) instead of a last-arriver reduce in the GEMM
         defer = self.DEFER_RESID and not tiled and splits > 1
