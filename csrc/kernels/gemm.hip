@@ -526,6 +526,48 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk)
   return *reinterpret_cast<const bf16x8*>(tile + row * 128 + pch * 16);
 }
 
+// Epilogue through LDS (free after the main loop's last barrier): the MFMA C
+// layout gives each lane 4 rows x 1 column, i.e. 2-4-byte scattered stores;
+// transposing the 128x128 fp32 tile through LDS turns every global store
+// into a 16-byte row-contiguous vector (256 B per 16 lanes).
+template <int EPI>
+__device__ __forceinline__ void tiled_epilogue(const GemmParams& p, f32x4 (&acc)[4][4], char* smem,
+                                               int m0, int n0, int split, int wm, int wn, int r,
+                                               int g) {
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        ct[(wm * 64 + i * 16 + 4 * g + q) * CT_LD + wn * 64 + j * 16 + r] = acc[i][j][q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < TBM * TBN / 8; c += 256) {
+    const int row = c >> 4, n = n0 + (c & 15) * 8, m = m0 + row;
+    if (m >= p.M || n >= p.N) continue;
+    const float* src = ct + row * CT_LD + (c & 15) * 8;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if constexpr (EPI == EPI_SILU_MUL) {
+      // interleaved [gate16 | up16] 32-column blocks: gate chunks pair with
+      // the up chunk 16 columns right, in the same tile
+      if ((c & 3) >= 2) continue;
+      const float* up = src + 16;
+      const f32x4 ulo = *reinterpret_cast<const f32x4*>(up);
+      const f32x4 uhi = *reinterpret_cast<const f32x4*>(up + 4);
+      const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
+      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
+    } else {
+      epilogue8<EPI>(p, m, n, v, split);
+    }
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM_TILED];  // [buf][A|W]; then C tile
@@ -579,42 +621,77 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles
     cur ^= 1;
   }
 
-  // Epilogue through LDS (free after the loop's last barrier): the MFMA C
-  // layout gives each lane 4 rows x 1 column, i.e. 2-4-byte scattered stores;
-  // transposing the 128x128 fp32 tile through LDS turns every global store
-  // into a 16-byte row-contiguous vector (256 B per 16 lanes).
-  float* ct = reinterpret_cast<float*>(smem);
+  tiled_epilogue<EPI>(p, acc, smem, m0, n0, split, wm, wn, r, g);
+}
+
+// 3-slot variant of the 128x128 kernel (decode-sized M, few tiles): the
+// two-buffer loop above drains every LDS-DMA at each __syncthreads, so one
+// k-step of MFMAs (~512 cycles) is all that covers a load's latency.  Here
+// step kt+2 is issued while kt computes: counted `s_waitcnt vmcnt(8|0)`
+// retires only this thread's step-kt loads (8 glds per step: 4 A + 4 W), one
+// raw s_barrier per step publishes them AND proves every wave finished step
+// kt-1, whose slot is then refilled (guide §5 "Pipelining across barriers").
+// 96 KiB of LDS: 1 block/CU, which the under-filled decode grids do not miss.
+constexpr int TILED3_SLOTS = 3;
+constexpr int SMEM_TILED3 = TBM * CT_LD * 4 > TILED3_SLOTS * 2 * TILE_BYTES ? TBM * CT_LD * 4
+                                                                           : TILED3_SLOTS * 2 * TILE_BYTES;
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_tiled3_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_TILED3];  // [slot][A|W]; then C tile
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int per_split = tiles_m * tiles_n;
+  const int split = bid / per_split;
+  const int t = bid % per_split;
+  const int tm = t % tiles_m, tn = t / tiles_m;
+  const int m0 = tm * TBM, n0 = tn * TBN;
+  const int KT = p.K / TBK;
+  const int kb = (int)((long)KT * split / p.splits), ke = (int)((long)KT * (split + 1) / p.splits);
+
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int r = lane & 15, g = lane >> 4;
+
+  f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int kt, int slot) {
+    char* b = smem + slot * 2 * TILE_BYTES;
+    stage_tile(b, p.A, p.lda, m0, p.M - 1, kt * TBK);
+    stage_tile(b + TILE_BYTES, p.W, p.ldw, n0, p.N - 1, kt * TBK);
+  };
+  constexpr int WAIT_ONE = 8 | (0x7 << 4) | (0xF << 8);  // vmcnt(8): next step's 8 glds stay in flight
+  constexpr int WAIT_ALL = (0x7 << 4) | (0xF << 8);      // vmcnt(0)
+  if (kb < ke) issue(kb, 0);
+  if (kb + 1 < ke) issue(kb + 1, 1);
+  int slot = 0;
+  for (int kt = kb; kt < ke; ++kt) {
+    if (kt + 1 < ke) __builtin_amdgcn_s_waitcnt(WAIT_ONE);
+    else __builtin_amdgcn_s_waitcnt(WAIT_ALL);
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < ke) issue(kt + 2, slot == 0 ? 2 : slot - 1);
+    const char* ta = smem + slot * 2 * TILE_BYTES;
+    const char* tw = ta + TILE_BYTES;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        ct[(wm * 64 + i * 16 + 4 * g + q) * CT_LD + wn * 64 + j * 16 + r] = acc[i][j][q];
-  __syncthreads();
-  for (int c = threadIdx.x; c < TBM * TBN / 8; c += 256) {
-    const int row = c >> 4, n = n0 + (c & 15) * 8, m = m0 + row;
-    if (m >= p.M || n >= p.N) continue;
-    const float* src = ct + row * CT_LD + (c & 15) * 8;
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
-    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    if constexpr (EPI == EPI_SILU_MUL) {
-      // interleaved [gate16 | up16] 32-column blocks: gate chunks pair with
-      // the up chunk 16 columns right, in the same tile
-      if ((c & 3) >= 2) continue;
-      const float* up = src + 16;
-      const f32x4 ulo = *reinterpret_cast<const f32x4*>(up);
-      const f32x4 uhi = *reinterpret_cast<const f32x4*>(up + 4);
-      const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
-      bf16x8 o;
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], wf[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
-      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
-    } else {
-      epilogue8<EPI>(p, m, n, v, split);
+      for (int i = 0; i < 4; ++i) af[i] = lds_frag(ta, wm * 64 + i * 16 + r, kk * 4 + g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wf[j] = lds_frag(tw, wn * 64 + j * 16 + r, kk * 4 + g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], wf[j], acc[i][j]);
     }
+    slot = slot == 2 ? 0 : slot + 1;
   }
+  __syncthreads();  // every wave's fragment reads retired before the C tile overwrites the slots
+  tiled_epilogue<EPI>(p, acc, smem, m0, n0, split, wm, wn, r, g);
 }
 
 // ---------------------------------------------------------------------------
@@ -834,6 +911,10 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m
 // Host launchers
 // ---------------------------------------------------------------------------
 static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
+// 128x128 launches of at most this many workgroups use the 3-slot ring kernel
+// (1 block/CU); larger grids keep the 2-blocks/CU double-buffered one.
+// lsd_gemm_set_tiled3_max(): tuning / tests; 0 = off
+static int g_tiled3_max_blocks = 0;
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
 // with N = H), M > g_sk_rows rows run as ceil(M / g_sk_rows) row blocks
@@ -902,7 +983,10 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
   }
   const int tm = (p.M + TBM - 1) / TBM, tn = (p.N + TBN - 1) / TBN;
   dim3 grid(tm * tn * p.splits), block(256);
-  hipLaunchKernelGGL((gemm_tiled_kernel<EPI>), grid, block, 0, st, p, tm, tn);
+  if (tm * tn * p.splits <= g_tiled3_max_blocks)
+    hipLaunchKernelGGL((gemm_tiled3_kernel<EPI>), grid, block, 0, st, p, tm, tn);
+  else
+    hipLaunchKernelGGL((gemm_tiled_kernel<EPI>), grid, block, 0, st, p, tm, tn);
   return hipGetLastError();
 }
 
@@ -911,6 +995,7 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
 using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
+extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" int lsd_gemm_sk_rblocks(int M, int N, int S) { return sk_rblocks(M, N, S); }
 extern "C" int lsd_gemm_sk_rows(int M, int N, int S) {  // rows per row block
   return sk_mt(M, sk_rblocks(M, N, S)) * 16;

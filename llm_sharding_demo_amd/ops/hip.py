@@ -98,18 +98,22 @@ class HipBackend(Backend):
     SK_ROWS = int(os.environ.get("LSD_SK_ROWS", "64"))
     # decode GEMM 128-column tiles above this many rows (off: slower, see gemm.hip)
     NW2_ROWS = int(os.environ.get("LSD_NW2_ROWS", str(1 << 30)))
+    # 128x128 launches of at most this many workgroups run the 3-slot LDS ring
+    # variant (step kt+2 in flight while kt computes; 1 block/CU); 0 = off
+    TILED3_MAX = int(os.environ.get("LSD_TILED3_MAX", "512"))
     # above 128 rows, GEMMs at least this wide go to the 128x128 tiled kernel
-    # (4 waves of 64x64 wave tiles, 100 workgroups for GPT-2 XL's MLP-up at 256
-    # rows) while narrower ones stay on split-K.  GPT-2 XL 2 x 256 (bench
-    # default), tok/s: all split-K 41.2-41.6k, MLP-up tiled (6400) 42.1-42.3k,
-    # + QKV tiled (4800) 40.7k, everything tiled (1600) 40.1k
-    # (profiles/r1_ab_tiled_min_n.log)
-    TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "6400"))
+    # (4 waves of 64x64 wave tiles) while narrower ones stay on split-K.
+    # GPT-2 XL 2 x 256 (bench default), tok/s, 4-step runs interleaved:
+    # all split-K 41.2-41.6k; MLP-up tiled (6400) 42.1-42.4k; + ring 42.5k;
+    # MLP-up and QKV tiled on the ring (4800) 42.8k; everything tiled (1600,
+    # double-buffered) 40.1k (profiles/r1_ab_tiled_min_n.log)
+    TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4800"))
 
     def __init__(self):
         self.C = _load()
         self.C.gemm_set_sk_rows(self.SK_ROWS)
         self.C.gemm_set_nw2_rows(self.NW2_ROWS)
+        self.C.gemm_set_tiled3_max(self.TILED3_MAX)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.counters = None
         self._rope = None

@@ -163,6 +163,43 @@ def test_gemm_large_prefill_shape(C, CNT):
 
 
 @pytest.fixture
+def TILED3(C):
+    """Route every 128x128 tiled launch to the 3-slot LDS ring variant."""
+    C.gemm_set_tiled3_max(1 << 30)
+    yield C
+    C.gemm_set_tiled3_max(0)
+
+
+@pytest.mark.parametrize("M", [100, 256, 300])
+@pytest.mark.parametrize("K", [64, 128, 192, 640])
+def test_tiled3_gemm_epilogues(TILED3, CNT, M, K):
+    """3-slot ring 128x128 kernel: every epilogue, M/N tails, 1, 2, 3 and 10
+    k-steps (fewer than, equal to and more than the ring), split-K slabs."""
+    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
+
+    C = TILED3
+    N = 320
+    a, w, bias = bf(M, K, seed=60), bf(N, K, scale=0.05, seed=61), bf(N, scale=0.1, seed=62)
+    y_ref = ref.linear(a, w, bias)
+    close(C.linear(a, w, bias, 0, True, 1, CNT), y_ref, 3e-2)
+    close(C.linear(a, w, bias, 1, True, 1, CNT), ref.gelu_new(y_ref), 3e-2)
+    w2 = w[:256].contiguous()
+    y = C.linear(a, interleave_gate_up(w2, 128).contiguous(), None, 2, True, 1, CNT)
+    close(y, ref.silu_mul(*ref.linear(a, w2).split(128, 1)), 3e-2)
+    close(C.linear_f32(a, w, True, 1, CNT), ref.linear(a, w), 2e-3, 1e-3)
+    x = torch.randn(M, N, device=DEV)
+    x_ref = x + y_ref
+    assert C.linear_residual(a, w, bias, x, 1, True, CNT, False) is None
+    close(x, x_ref, 2e-3, 1e-3)
+    if K >= 128:
+        x = torch.randn(M, N, device=DEV)
+        x_ref = x + y_ref
+        slab = C.linear_residual(a, w, bias, x, 2, True, CNT, False)
+        C.norm(x, slab, bias, None, None, 0.0, True, None, False)
+        close(x, x_ref, 2e-3, 1e-3)
+
+
+@pytest.fixture
 def BIG(C):
     """Force the pipelined 256x256 kernel for every tiled launch with M >= 256."""
     C.gemm_set_big_min(1)

@@ -351,6 +351,18 @@ def main():
             bench_gemm(M, V, H, label="_lmhead_tiled", force_tiled=True)
         bench_gemm(128, 128256, 4096, label="_lmhead_llama")
         bench_gemm(128, 128256, 4096, label="_lmhead_llama_tiled", force_tiled=True)
+    if "tiled3" in which:  # 128x128 kernel: double buffer vs 3-slot LDS ring, decode-sized M
+        for M in (128, 256):
+            for t3 in (0, 1 << 30):
+                C.gemm_set_tiled3_max(t3)
+                tag = "_ring3" if t3 else "_dbuf"
+                bench_gemm(M, 3 * H, H, label="_qkv_tiled" + tag, force_tiled=True)
+                bench_gemm(M, F, H, act=1, label="_fc_tiled" + tag, force_tiled=True)
+                bench_gemm(M, H, F, resid=True, label="_proj2_tiled" + tag, force_tiled=True)
+            bench_gemm(M, 3 * H, H, label="_qkv")
+            bench_gemm(M, F, H, act=1, label="_fc")
+            bench_gemm(M, H, F, resid=True, label="_proj2")
+        C.gemm_set_tiled3_max(0)
     if "tiledsk" in which:  # split-K slabs + norm combine: decode kernel vs 128x128 tiled
         for M in (64, 128):
             for (N, K, nm) in ((3 * H, H, "qkv"), (F, H, "fc"), (H, H, "proj"), (H, F, "proj2")):
