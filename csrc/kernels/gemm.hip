@@ -624,21 +624,25 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles
   tiled_epilogue<EPI>(p, acc, smem, m0, n0, split, wm, wn, r, g);
 }
 
-// 3-slot variant of the 128x128 kernel (decode-sized M, few tiles): the
+// Ring variant of the 128x128 kernel (decode-sized M, few tiles): the
 // two-buffer loop above drains every LDS-DMA at each __syncthreads, so one
-// k-step of MFMAs (~512 cycles) is all that covers a load's latency.  Here
-// step kt+2 is issued while kt computes: counted `s_waitcnt vmcnt(8|0)`
-// retires only this thread's step-kt loads (8 glds per step: 4 A + 4 W), one
-// raw s_barrier per step publishes them AND proves every wave finished step
-// kt-1, whose slot is then refilled (guide §5 "Pipelining across barriers").
-// 96 KiB of LDS: 1 block/CU, which the under-filled decode grids do not miss.
-constexpr int TILED3_SLOTS = 3;
-constexpr int SMEM_TILED3 = TBM * CT_LD * 4 > TILED3_SLOTS * 2 * TILE_BYTES ? TBM * CT_LD * 4
-                                                                           : TILED3_SLOTS * 2 * TILE_BYTES;
+// k-step of MFMAs (~512 cycles) is all that covers a load's latency.  Here a
+// ring of SLOTS k-steps keeps SLOTS-1 in flight while step kt computes:
+// counted `s_waitcnt vmcnt` retires only this thread's step-kt loads (8 glds
+// per step: 4 A + 4 W), one raw s_barrier per step publishes them AND proves
+// every wave finished step kt-1, whose slot is then refilled (guide §5
+// "Pipelining across barriers").  32 KiB per slot: 96 / 128 KiB, 1 block/CU,
+// which the under-filled decode grids do not miss.  Measured at 256 rows
+// (tools/microbench.py tiled3): QKV 26.1 -> 20.8 us, MLP-up 30.0 -> 24.1 us.
+template <int SLOTS>
+constexpr int smem_ring() {
+  return TBM * CT_LD * 4 > SLOTS * 2 * TILE_BYTES ? TBM * CT_LD * 4 : SLOTS * 2 * TILE_BYTES;
+}
 
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_tiled3_kernel(GemmParams p, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM_TILED3];  // [slot][A|W]; then C tile
+template <int EPI, int SLOTS>
+__global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int D = SLOTS - 1;  // prefetch distance (k-steps in flight)
+  __shared__ __attribute__((aligned(16))) char smem[smem_ring<SLOTS>()];  // [slot][A|W]; then C tile
   const int nwg = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int per_split = tiles_m * tiles_n;
@@ -664,16 +668,22 @@ __global__ __launch_bounds__(256) void gemm_tiled3_kernel(GemmParams p, int tile
     stage_tile(b, p.A, p.lda, m0, p.M - 1, kt * TBK);
     stage_tile(b + TILE_BYTES, p.W, p.ldw, n0, p.N - 1, kt * TBK);
   };
-  constexpr int WAIT_ONE = 8 | (0x7 << 4) | (0xF << 8);  // vmcnt(8): next step's 8 glds stay in flight
-  constexpr int WAIT_ALL = (0x7 << 4) | (0xF << 8);      // vmcnt(0)
-  if (kb < ke) issue(kb, 0);
-  if (kb + 1 < ke) issue(kb + 1, 1);
+  // vmcnt(8 n): the n later steps' glds stay in flight
+  constexpr int WAIT0 = (0x7 << 4) | (0xF << 8);
+  constexpr int WAIT1 = 8 | WAIT0;
+  constexpr int WAIT2 = 16 | WAIT0;
+  static_assert(SLOTS == 3 || SLOTS == 4, "ring of 3 or 4 slots");
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (kb + d < ke) issue(kb + d, d);
   int slot = 0;
   for (int kt = kb; kt < ke; ++kt) {
-    if (kt + 1 < ke) __builtin_amdgcn_s_waitcnt(WAIT_ONE);
-    else __builtin_amdgcn_s_waitcnt(WAIT_ALL);
+    const int later = min(D - 1, ke - 1 - kt);  // steps after kt already issued
+    if (later >= 2) __builtin_amdgcn_s_waitcnt(WAIT2);
+    else if (later == 1) __builtin_amdgcn_s_waitcnt(WAIT1);
+    else __builtin_amdgcn_s_waitcnt(WAIT0);
     __builtin_amdgcn_s_barrier();
-    if (kt + 2 < ke) issue(kt + 2, slot == 0 ? 2 : slot - 1);
+    if (kt + D < ke) issue(kt + D, slot == 0 ? SLOTS - 1 : slot - 1);
     const char* ta = smem + slot * 2 * TILE_BYTES;
     const char* tw = ta + TILE_BYTES;
 #pragma unroll
@@ -688,7 +698,7 @@ __global__ __launch_bounds__(256) void gemm_tiled3_kernel(GemmParams p, int tile
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], wf[j], acc[i][j]);
     }
-    slot = slot == 2 ? 0 : slot + 1;
+    slot = slot == SLOTS - 1 ? 0 : slot + 1;
   }
   __syncthreads();  // every wave's fragment reads retired before the C tile overwrites the slots
   tiled_epilogue<EPI>(p, acc, smem, m0, n0, split, wm, wn, r, g);
@@ -915,6 +925,7 @@ static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
 // (1 block/CU); larger grids keep the 2-blocks/CU double-buffered one.
 // lsd_gemm_set_tiled3_max(): tuning / tests; 0 = off
 static int g_tiled3_max_blocks = 0;
+static int g_ring_slots = 3;  // lsd_gemm_set_ring_slots(): 3 or 4
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
 // with N = H), M > g_sk_rows rows run as ceil(M / g_sk_rows) row blocks
@@ -983,8 +994,10 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
   }
   const int tm = (p.M + TBM - 1) / TBM, tn = (p.N + TBN - 1) / TBN;
   dim3 grid(tm * tn * p.splits), block(256);
-  if (tm * tn * p.splits <= g_tiled3_max_blocks)
-    hipLaunchKernelGGL((gemm_tiled3_kernel<EPI>), grid, block, 0, st, p, tm, tn);
+  if (tm * tn * p.splits <= g_tiled3_max_blocks && g_ring_slots == 4)
+    hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4>), grid, block, 0, st, p, tm, tn);
+  else if (tm * tn * p.splits <= g_tiled3_max_blocks)
+    hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3>), grid, block, 0, st, p, tm, tn);
   else
     hipLaunchKernelGGL((gemm_tiled_kernel<EPI>), grid, block, 0, st, p, tm, tn);
   return hipGetLastError();
@@ -996,6 +1009,7 @@ using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
+extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
 extern "C" int lsd_gemm_sk_rblocks(int M, int N, int S) { return sk_rblocks(M, N, S); }
 extern "C" int lsd_gemm_sk_rows(int M, int N, int S) {  // rows per row block
   return sk_mt(M, sk_rblocks(M, N, S)) * 16;

@@ -98,9 +98,13 @@ class HipBackend(Backend):
     SK_ROWS = int(os.environ.get("LSD_SK_ROWS", "64"))
     # decode GEMM 128-column tiles above this many rows (off: slower, see gemm.hip)
     NW2_ROWS = int(os.environ.get("LSD_NW2_ROWS", str(1 << 30)))
-    # 128x128 launches of at most this many workgroups run the 3-slot LDS ring
-    # variant (step kt+2 in flight while kt computes; 1 block/CU); 0 = off
-    TILED3_MAX = int(os.environ.get("LSD_TILED3_MAX", "512"))
+    # 128x128 launches of at most this many workgroups run the LDS ring variant
+    # (step kt+2 in flight while kt computes; 1 block/CU); 0 = off.  At 256
+    # rows QKV 25.8 -> 20.4 us, MLP-up 29.6 -> 23.3; lm_head's 393-tile grid
+    # at 128 rows is better on the 2-blocks/CU kernel (45.2 vs 47.7 us), and a
+    # 4-slot ring is slower everywhere (profiles/r1_microbench_ring_gemm.log)
+    TILED3_MAX = int(os.environ.get("LSD_TILED3_MAX", "256"))
+    RING_SLOTS = int(os.environ.get("LSD_RING_SLOTS", "3"))  # 3 or 4 (128 KiB of LDS)
     # above 128 rows, GEMMs at least this wide go to the 128x128 tiled kernel
     # (4 waves of 64x64 wave tiles) while narrower ones stay on split-K.
     # GPT-2 XL 2 x 256 (bench default), tok/s, 4-step runs interleaved:
@@ -114,6 +118,7 @@ class HipBackend(Backend):
         self.C.gemm_set_sk_rows(self.SK_ROWS)
         self.C.gemm_set_nw2_rows(self.NW2_ROWS)
         self.C.gemm_set_tiled3_max(self.TILED3_MAX)
+        self.C.gemm_set_ring_slots(self.RING_SLOTS)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.counters = None
         self._rope = None

@@ -162,22 +162,24 @@ def test_gemm_large_prefill_shape(C, CNT):
     close(C.linear(a, w, None, 0, True, 1, CNT), ref.linear(a, w), 3e-2)
 
 
-@pytest.fixture
-def TILED3(C):
-    """Route every 128x128 tiled launch to the 3-slot LDS ring variant."""
+@pytest.fixture(params=[3, 4])
+def RING(C, request):
+    """Route every 128x128 tiled launch to the LDS ring variant (3 or 4 slots)."""
     C.gemm_set_tiled3_max(1 << 30)
+    C.gemm_set_ring_slots(request.param)
     yield C
     C.gemm_set_tiled3_max(0)
+    C.gemm_set_ring_slots(3)
 
 
 @pytest.mark.parametrize("M", [100, 256, 300])
-@pytest.mark.parametrize("K", [64, 128, 192, 640])
-def test_tiled3_gemm_epilogues(TILED3, CNT, M, K):
-    """3-slot ring 128x128 kernel: every epilogue, M/N tails, 1, 2, 3 and 10
+@pytest.mark.parametrize("K", [64, 128, 192, 256, 640])
+def test_ring_gemm_epilogues(RING, CNT, M, K):
+    """Ring 128x128 kernel: every epilogue, M/N tails, 1, 2, 3, 4 and 10
     k-steps (fewer than, equal to and more than the ring), split-K slabs."""
     from llm_sharding_demo_amd.ops.hip import interleave_gate_up
 
-    C = TILED3
+    C = RING
     N = 320
     a, w, bias = bf(M, K, seed=60), bf(N, K, scale=0.05, seed=61), bf(N, scale=0.1, seed=62)
     y_ref = ref.linear(a, w, bias)

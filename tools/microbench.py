@@ -351,18 +351,32 @@ def main():
             bench_gemm(M, V, H, label="_lmhead_tiled", force_tiled=True)
         bench_gemm(128, 128256, 4096, label="_lmhead_llama")
         bench_gemm(128, 128256, 4096, label="_lmhead_llama_tiled", force_tiled=True)
+    if "fc256" in which:  # one shape for PMC passes: MLP-up at 256 rows, ring / dbuf / split-K
+        from llm_sharding_demo_amd.ops.hip import HipBackend
+        t3_default, minn_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N
+        for t3 in (1 << 30, 0):  # bench_gemm's HipBackend() applies the class knob
+            HipBackend.TILED3_MAX = t3
+            bench_gemm(256, F, H, act=1, label="_fc_tiled" + ("_ring3" if t3 else "_dbuf"), force_tiled=True)
+        HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N = t3_default, 1 << 30
+        bench_gemm(256, F, H, act=1, label="_fc_sk")
+        HipBackend.TILED_MIN_N = minn_default
     if "tiled3" in which:  # 128x128 kernel: double buffer vs 3-slot LDS ring, decode-sized M
+        from llm_sharding_demo_amd.ops.hip import HipBackend
+        t3_default, minn_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N
         for M in (128, 256):
-            for t3 in (0, 1 << 30):
-                C.gemm_set_tiled3_max(t3)
-                tag = "_ring3" if t3 else "_dbuf"
+            for t3, slots in ((0, 3), (1 << 30, 3), (1 << 30, 4)):  # bench_gemm's HipBackend() applies the class knobs
+                HipBackend.TILED3_MAX, HipBackend.RING_SLOTS = t3, slots
+                tag = f"_ring{slots}" if t3 else "_dbuf"
+                if M == 128:
+                    bench_gemm(M, V, H, label="_lmhead" + tag, force_tiled=True)
                 bench_gemm(M, 3 * H, H, label="_qkv_tiled" + tag, force_tiled=True)
                 bench_gemm(M, F, H, act=1, label="_fc_tiled" + tag, force_tiled=True)
                 bench_gemm(M, H, F, resid=True, label="_proj2_tiled" + tag, force_tiled=True)
-            bench_gemm(M, 3 * H, H, label="_qkv")
-            bench_gemm(M, F, H, act=1, label="_fc")
-            bench_gemm(M, H, F, resid=True, label="_proj2")
-        C.gemm_set_tiled3_max(0)
+            HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.RING_SLOTS = t3_default, 1 << 30, 3
+            bench_gemm(M, 3 * H, H, label="_qkv_sk")
+            bench_gemm(M, F, H, act=1, label="_fc_sk")
+            bench_gemm(M, H, F, resid=True, label="_proj2_sk")
+            HipBackend.TILED_MIN_N = minn_default
     if "tiledsk" in which:  # split-K slabs + norm combine: decode kernel vs 128x128 tiled
         for M in (64, 128):
             for (N, K, nm) in ((3 * H, H, "qkv"), (F, H, "fc"), (H, H, "proj"), (H, F, "proj2")):
