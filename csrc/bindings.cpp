@@ -20,6 +20,7 @@ hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws
 void lsd_gemm_set_big_min(int v);
 void lsd_gemm_set_tiled3_max(int v);
 void lsd_gemm_set_ring_slots(int v);
+void lsd_gemm_set_ring_tn(int v);
 void lsd_attn_set_max_wg(int v);
 int lsd_gemm_sk_rows(int M, int N, int S);
 int lsd_gemm_sk_rblocks(int M, int N, int S);
@@ -411,6 +412,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_big_min", [](int64_t v) { lsd_gemm_set_big_min((int)v); });
   m.def("gemm_set_tiled3_max", [](int64_t v) { lsd_gemm_set_tiled3_max((int)v); });
   m.def("gemm_set_ring_slots", [](int64_t v) { lsd_gemm_set_ring_slots((int)v); });
+  m.def("gemm_set_ring_tn", [](int64_t v) { lsd_gemm_set_ring_tn((int)v); });
   // decode attention: cap the grid (blocks loop over (sequence, head) items)
   m.def("attn_set_max_wg", [](int64_t v) { lsd_attn_set_max_wg((int)v); });
   // decode GEMM: rows per row block (M above it runs as several row blocks)

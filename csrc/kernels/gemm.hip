@@ -506,12 +506,14 @@ typedef __attribute__((address_space(1))) const void gbl_cvoid;
 // the 16-B chunk index XOR-swizzled by (row>>1)&7.  glds writes lane-linear
 // (base + 16*lane), so the swizzle goes on the per-lane SOURCE address and the
 // same XOR is applied on the read (guide §5.4 rule 21).
+template <int ROWS = TBM>
 __device__ __forceinline__ void stage_tile(char* lds_tile, const bf16* src, long ld, int row0,
                                            int row_max, int k0) {
   const int lane = lane_id(), w = threadIdx.x >> 6;
+  constexpr int PER_WAVE = ROWS / 32;  // wave-instructions of 1 KiB (8 rows of 64 k) per wave
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int inst = w * 4 + q;           // 16 wave-instructions of 1 KiB per tile
+  for (int q = 0; q < PER_WAVE; ++q) {
+    const int inst = w * PER_WAVE + q;
     const int row = inst * 8 + (lane >> 3);
     const int pch = lane & 7;
     const int lch = pch ^ ((row >> 1) & 7);
@@ -530,23 +532,27 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk)
 // layout gives each lane 4 rows x 1 column, i.e. 2-4-byte scattered stores;
 // transposing the 128x128 fp32 tile through LDS turns every global store
 // into a 16-byte row-contiguous vector (256 B per 16 lanes).
-template <int EPI>
-__device__ __forceinline__ void tiled_epilogue(const GemmParams& p, f32x4 (&acc)[4][4], char* smem,
+// TN = tile columns (128, or 64 for the narrow ring tiles); wave (wm, wn)
+// holds rows wm*64 + [0, 64) and columns wn*TN/2 + [0, TN/2).
+template <int EPI, int TN = TBN>
+__device__ __forceinline__ void tiled_epilogue(const GemmParams& p, f32x4 (&acc)[4][TN / 32], char* smem,
                                                int m0, int n0, int split, int wm, int wn, int r,
                                                int g) {
+  constexpr int CLD = TN + 4;  // bank skew
+  constexpr int CPR = TN / 8;  // 8-column chunks per row
   float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < TN / 32; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        ct[(wm * 64 + i * 16 + 4 * g + q) * CT_LD + wn * 64 + j * 16 + r] = acc[i][j][q];
+        ct[(wm * 64 + i * 16 + 4 * g + q) * CLD + wn * (TN / 2) + j * 16 + r] = acc[i][j][q];
   __syncthreads();
-  for (int c = threadIdx.x; c < TBM * TBN / 8; c += 256) {
-    const int row = c >> 4, n = n0 + (c & 15) * 8, m = m0 + row;
+  for (int c = threadIdx.x; c < TBM * CPR; c += 256) {
+    const int row = c / CPR, n = n0 + (c % CPR) * 8, m = m0 + row;
     if (m >= p.M || n >= p.N) continue;
-    const float* src = ct + row * CT_LD + (c & 15) * 8;
+    const float* src = ct + row * CLD + (c % CPR) * 8;
     const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
     const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -634,22 +640,29 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles
 // "Pipelining across barriers").  32 KiB per slot: 96 / 128 KiB, 1 block/CU,
 // which the under-filled decode grids do not miss.  Measured at 256 rows
 // (tools/microbench.py tiled3): QKV 26.1 -> 20.8 us, MLP-up 30.0 -> 24.1 us.
-template <int SLOTS>
+template <int SLOTS, int TN>
 constexpr int smem_ring() {
-  return TBM * CT_LD * 4 > SLOTS * 2 * TILE_BYTES ? TBM * CT_LD * 4 : SLOTS * 2 * TILE_BYTES;
+  return TBM * (TN + 4) * 4 > SLOTS * (TILE_BYTES + TN * TBK * 2) ? TBM * (TN + 4) * 4
+                                                                 : SLOTS * (TILE_BYTES + TN * TBK * 2);
 }
 
-template <int EPI, int SLOTS>
+// s_waitcnt immediate for vmcnt(n) alone (gfx9 layout: vmcnt[3:0] | vmcnt[5:4] << 14)
+constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+
+template <int EPI, int SLOTS, int TN>
 __global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_m, int tiles_n) {
-  constexpr int D = SLOTS - 1;  // prefetch distance (k-steps in flight)
-  __shared__ __attribute__((aligned(16))) char smem[smem_ring<SLOTS>()];  // [slot][A|W]; then C tile
+  constexpr int D = SLOTS - 1;                    // prefetch distance (k-steps in flight)
+  constexpr int JT = TN / 32;                     // 16-column MFMA tiles per wave
+  constexpr int SLOT_BYTES = TILE_BYTES + TN * TBK * 2;
+  constexpr int LPS = 4 + TN / 32;                // glds per thread per k-step (A + W)
+  __shared__ __attribute__((aligned(16))) char smem[smem_ring<SLOTS, TN>()];  // [slot][A|W]; then C tile
   const int nwg = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int per_split = tiles_m * tiles_n;
   const int split = bid / per_split;
   const int t = bid % per_split;
   const int tm = t % tiles_m, tn = t / tiles_m;
-  const int m0 = tm * TBM, n0 = tn * TBN;
+  const int m0 = tm * TBM, n0 = tn * TN;
   const int KT = p.K / TBK;
   const int kb = (int)((long)KT * split / p.splits), ke = (int)((long)KT * (split + 1) / p.splits);
 
@@ -657,51 +670,48 @@ __global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_
   const int wm = w >> 1, wn = w & 1;
   const int r = lane & 15, g = lane >> 4;
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][JT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto issue = [&](int kt, int slot) {
-    char* b = smem + slot * 2 * TILE_BYTES;
-    stage_tile(b, p.A, p.lda, m0, p.M - 1, kt * TBK);
-    stage_tile(b + TILE_BYTES, p.W, p.ldw, n0, p.N - 1, kt * TBK);
+    char* b = smem + slot * SLOT_BYTES;
+    stage_tile<TBM>(b, p.A, p.lda, m0, p.M - 1, kt * TBK);
+    stage_tile<TN>(b + TILE_BYTES, p.W, p.ldw, n0, p.N - 1, kt * TBK);
   };
-  // vmcnt(8 n): the n later steps' glds stay in flight
-  constexpr int WAIT0 = (0x7 << 4) | (0xF << 8);
-  constexpr int WAIT1 = 8 | WAIT0;
-  constexpr int WAIT2 = 16 | WAIT0;
   static_assert(SLOTS == 3 || SLOTS == 4, "ring of 3 or 4 slots");
+  static_assert(2 * LPS <= 63, "vmcnt holds at most 63 outstanding loads");
 #pragma unroll
   for (int d = 0; d < D; ++d)
     if (kb + d < ke) issue(kb + d, d);
   int slot = 0;
   for (int kt = kb; kt < ke; ++kt) {
     const int later = min(D - 1, ke - 1 - kt);  // steps after kt already issued
-    if (later >= 2) __builtin_amdgcn_s_waitcnt(WAIT2);
-    else if (later == 1) __builtin_amdgcn_s_waitcnt(WAIT1);
-    else __builtin_amdgcn_s_waitcnt(WAIT0);
+    if (later >= 2) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * LPS));
+    else if (later == 1) __builtin_amdgcn_s_waitcnt(vmcnt_imm(LPS));
+    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
     __builtin_amdgcn_s_barrier();
     if (kt + D < ke) issue(kt + D, slot == 0 ? SLOTS - 1 : slot - 1);
-    const char* ta = smem + slot * 2 * TILE_BYTES;
+    const char* ta = smem + slot * SLOT_BYTES;
     const char* tw = ta + TILE_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], wf[4];
+      bf16x8 af[4], wf[JT];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = lds_frag(ta, wm * 64 + i * 16 + r, kk * 4 + g);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wf[j] = lds_frag(tw, wn * 64 + j * 16 + r, kk * 4 + g);
+      for (int j = 0; j < JT; ++j) wf[j] = lds_frag(tw, wn * (TN / 2) + j * 16 + r, kk * 4 + g);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], wf[j], acc[i][j]);
+        for (int j = 0; j < JT; ++j) acc[i][j] = mfma16(af[i], wf[j], acc[i][j]);
     }
     slot = slot == SLOTS - 1 ? 0 : slot + 1;
   }
   __syncthreads();  // every wave's fragment reads retired before the C tile overwrites the slots
-  tiled_epilogue<EPI>(p, acc, smem, m0, n0, split, wm, wn, r, g);
+  tiled_epilogue<EPI, TN>(p, acc, smem, m0, n0, split, wm, wn, r, g);
 }
 
 // ---------------------------------------------------------------------------
@@ -926,6 +936,7 @@ static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
 // lsd_gemm_set_tiled3_max(): tuning / tests; 0 = off
 static int g_tiled3_max_blocks = 0;
 static int g_ring_slots = 3;  // lsd_gemm_set_ring_slots(): 3 or 4
+static int g_ring_tn = 128;   // lsd_gemm_set_ring_tn(): ring tile columns, 128 or 64
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
 // with N = H), M > g_sk_rows rows run as ceil(M / g_sk_rows) row blocks
@@ -992,12 +1003,20 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
     hipLaunchKernelGGL((gemm_big_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn);
     return hipGetLastError();
   }
-  const int tm = (p.M + TBM - 1) / TBM, tn = (p.N + TBN - 1) / TBN;
+  const int tm = (p.M + TBM - 1) / TBM;
+  if (g_ring_tn == 64) {  // narrow ring tiles: twice the workgroups of the 128-column grid
+    const int tn = (p.N + 63) / 64;
+    if (tm * tn * p.splits <= g_tiled3_max_blocks) {
+      hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 64>), dim3(tm * tn * p.splits), dim3(256), 0, st, p, tm, tn);
+      return hipGetLastError();
+    }
+  }
+  const int tn = (p.N + TBN - 1) / TBN;
   dim3 grid(tm * tn * p.splits), block(256);
   if (tm * tn * p.splits <= g_tiled3_max_blocks && g_ring_slots == 4)
-    hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4>), grid, block, 0, st, p, tm, tn);
+    hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 128>), grid, block, 0, st, p, tm, tn);
   else if (tm * tn * p.splits <= g_tiled3_max_blocks)
-    hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3>), grid, block, 0, st, p, tm, tn);
+    hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 128>), grid, block, 0, st, p, tm, tn);
   else
     hipLaunchKernelGGL((gemm_tiled_kernel<EPI>), grid, block, 0, st, p, tm, tn);
   return hipGetLastError();
@@ -1010,6 +1029,7 @@ using namespace lsd;
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
+extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = v == 64 ? 64 : 128; }
 extern "C" int lsd_gemm_sk_rblocks(int M, int N, int S) { return sk_rblocks(M, N, S); }
 extern "C" int lsd_gemm_sk_rows(int M, int N, int S) {  // rows per row block
   return sk_mt(M, sk_rblocks(M, N, S)) * 16;

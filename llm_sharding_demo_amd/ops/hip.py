@@ -98,20 +98,27 @@ class HipBackend(Backend):
     SK_ROWS = int(os.environ.get("LSD_SK_ROWS", "64"))
     # decode GEMM 128-column tiles above this many rows (off: slower, see gemm.hip)
     NW2_ROWS = int(os.environ.get("LSD_NW2_ROWS", str(1 << 30)))
-    # 128x128 launches of at most this many workgroups run the LDS ring variant
-    # (step kt+2 in flight while kt computes; 1 block/CU); 0 = off.  At 256
-    # rows QKV 25.8 -> 20.4 us, MLP-up 29.6 -> 23.3; lm_head's 393-tile grid
-    # at 128 rows is better on the 2-blocks/CU kernel (45.2 vs 47.7 us), and a
-    # 4-slot ring is slower everywhere (profiles/r1_microbench_ring_gemm.log)
+    # tiled launches of at most this many workgroups run the LDS ring variant
+    # (steps kt+1, kt+2 in flight while kt computes; 1 block/CU); 0 = off.  At
+    # 256 rows and 128x128 tiles QKV 25.8 -> 20.4 us, MLP-up 29.6 -> 23.3;
+    # lm_head's 393-tile grid at 128 rows is better on the 2-blocks/CU kernel
+    # (45.2 vs 47.7 us); 4 slots = 3 slots (profiles/r1_ab_ring_n64.log)
     TILED3_MAX = int(os.environ.get("LSD_TILED3_MAX", "256"))
     RING_SLOTS = int(os.environ.get("LSD_RING_SLOTS", "3"))  # 3 or 4 (128 KiB of LDS)
-    # above 128 rows, GEMMs at least this wide go to the 128x128 tiled kernel
+    # ring tile columns, 128 or 64.  128x64 tiles double the workgroups of the
+    # decode-sized grids: at 256 rows QKV 20.5 -> 15.6 us, MLP-up 23.5 -> 17.3
+    # (split-K kernel 23.3 / 26.2, hipBLASLt 19.3 / 20.0); bench 42.9k -> 43.8k
+    RING_TN = int(os.environ.get("LSD_RING_TN", "64"))
+    # above TILED_MIN_M rows, GEMMs at least this wide go to the tiled kernels
     # (4 waves of 64x64 wave tiles) while narrower ones stay on split-K.
     # GPT-2 XL 2 x 256 (bench default), tok/s, 4-step runs interleaved:
     # all split-K 41.2-41.6k; MLP-up tiled (6400) 42.1-42.4k; + ring 42.5k;
     # MLP-up and QKV tiled on the ring (4800) 42.8k; everything tiled (1600,
     # double-buffered) 40.1k (profiles/r1_ab_tiled_min_n.log)
     TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4800"))
+    # ... above this many rows.  At 128 rows (2 x 128 microbatches): GPT-2 XL
+    # 33.8k either way, Llama-3 8B 17.0k -> 18.0k tok/s with 64
+    TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
 
     def __init__(self):
         self.C = _load()
@@ -119,6 +126,7 @@ class HipBackend(Backend):
         self.C.gemm_set_nw2_rows(self.NW2_ROWS)
         self.C.gemm_set_tiled3_max(self.TILED3_MAX)
         self.C.gemm_set_ring_slots(self.RING_SLOTS)
+        self.C.gemm_set_ring_tn(self.RING_TN)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.counters = None
         self._rope = None
@@ -164,7 +172,7 @@ class HipBackend(Backend):
     # ------------------------------------------------------------------
     @classmethod
     def _tiled(cls, M: int, N: int = 0) -> bool:
-        return M > cls.SK_MAX_M or (M > 128 and N >= cls.TILED_MIN_N)
+        return M > cls.SK_MAX_M or (M > cls.TILED_MIN_M and N >= cls.TILED_MIN_N)
 
     def _resid_splits(self, M: int, N: int, K: int) -> int:
         if self._tiled(M, N):

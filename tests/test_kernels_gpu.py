@@ -162,14 +162,18 @@ def test_gemm_large_prefill_shape(C, CNT):
     close(C.linear(a, w, None, 0, True, 1, CNT), ref.linear(a, w), 3e-2)
 
 
-@pytest.fixture(params=[3, 4])
+@pytest.fixture(params=[(3, 128), (4, 128), (3, 64)])
 def RING(C, request):
-    """Route every 128x128 tiled launch to the LDS ring variant (3 or 4 slots)."""
+    """Route every tiled launch to the LDS ring variant: 3 or 4 slots of
+    128x128 tiles, or 3 slots of 128x64 tiles."""
+    slots, tn = request.param
     C.gemm_set_tiled3_max(1 << 30)
-    C.gemm_set_ring_slots(request.param)
+    C.gemm_set_ring_slots(slots)
+    C.gemm_set_ring_tn(tn)
     yield C
     C.gemm_set_tiled3_max(0)
     C.gemm_set_ring_slots(3)
+    C.gemm_set_ring_tn(128)
 
 
 @pytest.mark.parametrize("M", [100, 256, 300])
@@ -180,7 +184,7 @@ def test_ring_gemm_epilogues(RING, CNT, M, K):
     from llm_sharding_demo_amd.ops.hip import interleave_gate_up
 
     C = RING
-    N = 320
+    N = 352  # 2.75 tiles of 128 columns, 5.5 of 64: a partial last tile either way
     a, w, bias = bf(M, K, seed=60), bf(N, K, scale=0.05, seed=61), bf(N, scale=0.1, seed=62)
     y_ref = ref.linear(a, w, bias)
     close(C.linear(a, w, bias, 0, True, 1, CNT), y_ref, 3e-2)

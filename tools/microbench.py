@@ -364,15 +364,17 @@ def main():
         from llm_sharding_demo_amd.ops.hip import HipBackend
         t3_default, minn_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N
         for M in (128, 256):
-            for t3, slots in ((0, 3), (1 << 30, 3), (1 << 30, 4)):  # bench_gemm's HipBackend() applies the class knobs
-                HipBackend.TILED3_MAX, HipBackend.RING_SLOTS = t3, slots
-                tag = f"_ring{slots}" if t3 else "_dbuf"
+            for t3, slots, rtn in ((0, 3, 128), (1 << 30, 3, 128), (1 << 30, 4, 128), (1 << 30, 3, 64)):
+                # bench_gemm's HipBackend() applies the class knobs
+                HipBackend.TILED3_MAX, HipBackend.RING_SLOTS, HipBackend.RING_TN = t3, slots, rtn
+                tag = (f"_ring{slots}" + ("_n64" if rtn == 64 else "")) if t3 else "_dbuf"
                 if M == 128:
                     bench_gemm(M, V, H, label="_lmhead" + tag, force_tiled=True)
                 bench_gemm(M, 3 * H, H, label="_qkv_tiled" + tag, force_tiled=True)
                 bench_gemm(M, F, H, act=1, label="_fc_tiled" + tag, force_tiled=True)
                 bench_gemm(M, H, F, resid=True, label="_proj2_tiled" + tag, force_tiled=True)
             HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.RING_SLOTS = t3_default, 1 << 30, 3
+            HipBackend.RING_TN = 128
             bench_gemm(M, 3 * H, H, label="_qkv_sk")
             bench_gemm(M, F, H, act=1, label="_fc_sk")
             bench_gemm(M, H, F, resid=True, label="_proj2_sk")
