@@ -109,16 +109,17 @@ class HipBackend(Backend):
     # decode-sized grids: at 256 rows QKV 20.5 -> 15.6 us, MLP-up 23.5 -> 17.3
     # (split-K kernel 23.3 / 26.2, hipBLASLt 19.3 / 20.0); bench 42.9k -> 43.8k
     RING_TN = int(os.environ.get("LSD_RING_TN", "64"))
-    # above TILED_MIN_M rows, GEMMs at least this wide go to the tiled kernels
-    # (4 waves of 64x64 wave tiles) while narrower ones stay on split-K.
-    # GPT-2 XL 2 x 256 (bench default), tok/s, 4-step runs interleaved:
-    # all split-K 41.2-41.6k; MLP-up tiled (6400) 42.1-42.4k; + ring 42.5k;
-    # MLP-up and QKV tiled on the ring (4800) 42.8k; everything tiled (1600,
-    # double-buffered) 40.1k (profiles/r1_ab_tiled_min_n.log)
-    TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4800"))
-    # ... above this many rows.  At 128 rows (2 x 128 microbatches): GPT-2 XL
-    # 33.8k either way, Llama-3 8B 17.0k -> 18.0k tok/s with 64
+    # Decode GEMMs leave split-K for the tiled kernels (the 128x64 LDS ring at
+    # these grid sizes) above TILED_ALL_M rows at any width, and above
+    # TILED_MIN_M rows when at least TILED_MIN_N wide.  bench tok/s (1 MI355X,
+    # profiles/r1_ab_tiled_min_n.log, r1_ab_ring_n64.log):
+    #   GPT-2 XL 2 x 256: split-K 41.2-41.6k; MLP-up + QKV tiled 43.8k; all 46.3-46.6k
+    #   GPT-2 small 2 x 256: split-K 286.8k; all tiled 309.8k
+    #   GPT-2 XL 2 x 128: split-K 34.0k; all tiled 33.3k (N = 1600 prefers split-K at 128 rows)
+    #   Llama-3 8B 2 x 128: split-K 17.0k; >= 4800 wide 18.0-18.2k; all (N >= 4096) 18.7k
+    TILED_ALL_M = int(os.environ.get("LSD_TILED_ALL_M", "128"))
     TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
+    TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4000"))
 
     def __init__(self):
         self.C = _load()
@@ -172,10 +173,16 @@ class HipBackend(Backend):
     # ------------------------------------------------------------------
     @classmethod
     def _tiled(cls, M: int, N: int = 0) -> bool:
-        return M > cls.SK_MAX_M or (M > cls.TILED_MIN_M and N >= cls.TILED_MIN_N)
+        return (M > cls.SK_MAX_M or M > cls.TILED_ALL_M
+                or (M > cls.TILED_MIN_M and N >= cls.TILED_MIN_N))
 
     def _resid_splits(self, M: int, N: int, K: int) -> int:
         if self._tiled(M, N):
+            if M <= self.SK_MAX_M and self.TILED3_MAX and self.RING_TN == 64:
+                # decode rows on the 128x64 ring: as many splits as keep the
+                # grid on the ring kernel
+                tiles = math.ceil(M / 128) * math.ceil(N / 64)
+                return max(1, min(self.TILED3_MAX // tiles, K // 64 // 2 or 1))
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
             return max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
         if self.DEFER_RESID:

@@ -353,16 +353,16 @@ def main():
         bench_gemm(128, 128256, 4096, label="_lmhead_llama_tiled", force_tiled=True)
     if "fc256" in which:  # one shape for PMC passes: MLP-up at 256 rows, ring / dbuf / split-K
         from llm_sharding_demo_amd.ops.hip import HipBackend
-        t3_default, minn_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N
+        t3_default, minn_default, allm_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M
         for t3 in (1 << 30, 0):  # bench_gemm's HipBackend() applies the class knob
             HipBackend.TILED3_MAX = t3
             bench_gemm(256, F, H, act=1, label="_fc_tiled" + ("_ring3" if t3 else "_dbuf"), force_tiled=True)
-        HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N = t3_default, 1 << 30
+        HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M = t3_default, 1 << 30, 1 << 30
         bench_gemm(256, F, H, act=1, label="_fc_sk")
-        HipBackend.TILED_MIN_N = minn_default
+        HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M = minn_default, allm_default
     if "tiled3" in which:  # 128x128 kernel: double buffer vs 3-slot LDS ring, decode-sized M
         from llm_sharding_demo_amd.ops.hip import HipBackend
-        t3_default, minn_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N
+        t3_default, minn_default, allm_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M
         for M in (128, 256):
             for t3, slots, rtn in ((0, 3, 128), (1 << 30, 3, 128), (1 << 30, 4, 128), (1 << 30, 3, 64)):
                 # bench_gemm's HipBackend() applies the class knobs
@@ -374,11 +374,12 @@ def main():
                 bench_gemm(M, F, H, act=1, label="_fc_tiled" + tag, force_tiled=True)
                 bench_gemm(M, H, F, resid=True, label="_proj2_tiled" + tag, force_tiled=True)
             HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.RING_SLOTS = t3_default, 1 << 30, 3
+            HipBackend.TILED_ALL_M = 1 << 30
             HipBackend.RING_TN = 128
             bench_gemm(M, 3 * H, H, label="_qkv_sk")
             bench_gemm(M, F, H, act=1, label="_fc_sk")
             bench_gemm(M, H, F, resid=True, label="_proj2_sk")
-            HipBackend.TILED_MIN_N = minn_default
+            HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M = minn_default, allm_default
     if "tiledsk" in which:  # split-K slabs + norm combine: decode kernel vs 128x128 tiled
         for M in (64, 128):
             for (N, K, nm) in ((3 * H, H, "qkv"), (F, H, "fc"), (H, H, "proj"), (H, F, "proj2")):
