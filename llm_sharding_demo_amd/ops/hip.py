@@ -118,6 +118,8 @@ class HipBackend(Backend):
     #   GPT-2 XL 2 x 128: split-K 34.0k; all tiled 33.3k (N = 1600 prefers split-K at 128 rows)
     #   Llama-3 8B 2 x 128: split-K 17.0k; >= 4800 wide 18.0-18.2k; all (N >= 4096) 18.7k
     TILED_ALL_M = int(os.environ.get("LSD_TILED_ALL_M", "128"))
+    # workgroup target of split-K residual GEMMs on the ring (0 = TILED3_MAX)
+    RING_RESID_TARGET = int(os.environ.get("LSD_RING_RESID_TARGET", "0"))
     TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
     TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4000"))
 
@@ -182,7 +184,8 @@ class HipBackend(Backend):
                 # decode rows on the 128x64 ring: as many splits as keep the
                 # grid on the ring kernel
                 tiles = math.ceil(M / 128) * math.ceil(N / 64)
-                return max(1, min(self.TILED3_MAX // tiles, K // 64 // 2 or 1))
+                target = min(self.TILED3_MAX, self.RING_RESID_TARGET or self.TILED3_MAX)
+                return max(1, min(target // tiles, K // 64 // 2 or 1))
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
             return max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
         if self.DEFER_RESID:
