@@ -120,17 +120,25 @@ def make_plan(cfg: ModelConfig, num_stages: int, split_points: Optional[Sequence
 #
 # The cost model is decode time per microbatch per step (us) on MI355X,
 # calibrated against the kernel profile and microbenchmarks of the bench
-# config (profiles/r1_xl_*_kernel_stats.csv, r1_microbench_*; 128-row
-# microbatches, GPT-2 XL: attention half ~70 us, MLP half ~47 us, head ~146 us):
-#   decode GEMM  ~ 5 us + weight bytes / 1.3 TB/s + FLOPs / 2 PF; QKV + 6 us
-#                (KV-cache scatter, RoPE); lm_head (tiled kernel) 5 us +
-#                bytes / 4.4 TB/s
-#   attention    ~ 3 us + KV bytes / 6 TB/s
-#   norm 6 us, sampler 8 us + 0.37 us/row, embed 4 us.
+# configs (kernel-trace averages with the other microbatch lane running).
+# Up to 64 rows (split-K decode GEMMs; profiles/r1_xl_*_kernel_stats.csv,
+# r1_microbench_*):
+#   decode GEMM  ~ 5 us + weight bytes / 1.3 TB/s + FLOPs / 2 PF
+#   lm_head      ~ 5 us + bytes / 4.4 TB/s (128x128 tiled kernel)
+# Above 64 rows (LDS-ring / big tiled GEMMs; profiles/r1_xl_b512_kernel_stats_v5.csv,
+# GPT-2 XL 2 x 256: attention half 86.7 us, MLP half 36.5 us, head 138.8 us):
+#   decode GEMM  ~ 6 us + FLOPs / 0.45 PF;  lm_head ~ 5 us + FLOPs / 0.55 PF
+# Both: QKV + 6 us (KV-cache scatter, RoPE); attention ~ 3 us + KV bytes /
+# 6 TB/s; norm 6 us; sampler 8 us + 0.37 us/row up to 128 rows (flat above:
+# 57 us at 256 rows); embed 4 us.
 UnitPlan = List[Tuple[int, int]]
 
 
 def _gemm_us(n: int, k: int, rows: int) -> float:
+    if rows > 64:
+        if n >= 16384:  # vocab projection
+            return 5.0 + 2.0 * rows * n * k / 0.55e9
+        return 6.0 + 2.0 * rows * n * k / 0.45e9  # FLOPs per us
     if n >= 16384:  # vocab projection on the 128x128 tiled kernel
         return 5.0 + n * k * 2 / 4.4e6
     return 5.0 + n * k * 2 / 1.3e6 + 2.0 * rows * n * k / 2.0e9  # bytes, FLOPs per us
@@ -147,7 +155,7 @@ def unit_costs(cfg: ModelConfig, rows: int = 128, avg_ctx: int = 192) -> Tuple[L
         up = _gemm_us(2 * cfg.ffn, h, rows)
     a = norm + _gemm_us(cfg.qkv_size, h, rows) + 6.0 + attn + _gemm_us(h, cfg.q_size, rows)
     m = norm + up + _gemm_us(h, cfg.ffn, rows)
-    head = norm + _gemm_us(cfg.vocab_padded, h, rows) + 8.0 + 0.37 * rows
+    head = norm + _gemm_us(cfg.vocab_padded, h, rows) + 8.0 + 0.37 * min(rows, 128)
     embed = 4.0
     return [a, m] * cfg.n_layers, head, embed
 
@@ -214,7 +222,7 @@ def make_unit_plan(cfg: ModelConfig, num_stages: int, split_points: Optional[Seq
     elif P == 1:
         plan = [(0, 2 * L)]
     else:
-        costs, head, embed = unit_costs(cfg, max(1, min(rows, 128)), avg_ctx)
+        costs, head, embed = unit_costs(cfg, max(1, min(rows, 256)), avg_ctx)
         if half_layers:
             plan = _native_or_python_dp(costs, P, head, embed)
         else:
