@@ -44,6 +44,34 @@ def test_stage_logits_match_cpu_golden(model):
         torch.testing.assert_close(dg[:, : mc.vocab_size].cpu(), dc, atol=0.05, rtol=0.05)
 
 
+@pytest.mark.parametrize("model", ["gpt2-test", "llama-test"])
+def test_wide_decode_batch_on_ring_gemms_matches_cpu_golden(model):
+    """200 decode rows: every decode GEMM (QKV + KV append, MLP, residual
+    split-K slabs) leaves the split-K kernel for the 128x64 LDS-ring GEMM."""
+    import random
+
+    from llm_sharding_demo_amd.ops.hip import HipBackend
+
+    assert HipBackend._tiled(200, 64) and HipBackend.TILED3_MAX > 0
+    mc = get_model_config(model)
+    w = full_weights(mc)
+    B = 200
+    cpu = StageModel(mc, 0, mc.n_layers, True, True, weights=w, max_slots=B, max_seq=64)
+    gpu = StageModel(mc, 0, mc.n_layers, True, True, device="cuda", weights=w, max_slots=B, max_seq=64)
+    rnd = random.Random(7)
+    prompts = [[rnd.randrange(1, 200) for _ in range(rnd.randrange(2, 12))] for _ in range(B)]
+    slots = list(range(B))
+    flat = torch.tensor([t for p in prompts for t in p], dtype=torch.int32)
+    cpu.forward(BatchMeta.build(slots, [0] * B, [len(p) for p in prompts], "cpu"), flat)
+    gpu.forward(BatchMeta.build(slots, [0] * B, [len(p) for p in prompts], "cuda"), flat.cuda())
+    for step in range(2):
+        toks = torch.tensor([rnd.randrange(1, 200) for _ in range(B)], dtype=torch.int32)
+        pos = [len(p) + step for p in prompts]
+        dc = cpu.forward(BatchMeta.decode(slots, pos, "cpu", max(pos) + 1), toks)[:, : mc.vocab_size]
+        dg = gpu.forward(BatchMeta.decode(slots, pos, "cuda", max(pos) + 1), toks.cuda())
+        torch.testing.assert_close(dg[:, : mc.vocab_size].cpu(), dc, atol=0.05, rtol=0.05)
+
+
 def _engine(model, P=1, graphs=True, **kw):
     cfg = EngineConfig(model_id=model, num_stages=P, max_batch=16, device="cuda", use_graphs=graphs,
                        max_seq_len=512, **kw)
