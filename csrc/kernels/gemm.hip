@@ -5,17 +5,21 @@
 // `server.py:102`).  Weights are stored [N][K] (K-contiguous) so a
 // 16x16x32 B-operand fragment is one 16-byte load.
 //
-// Two kernels:
-//  * gemm_sk      -- M <= 64 (decode microbatches).  Weight-bandwidth bound:
+// Four kernels:
+//  * gemm_sk      -- decode microbatches (M <= 64; narrow GEMMs to 128 rows).  Weight-bandwidth bound:
 //    W streamed HBM -> VGPRs (read once, no LDS round trip), the small A
 //    operand staged through LDS with full-line LDS-DMA, split-K across
 //    workgroups for occupancy with an in-kernel last-arriver combine that
 //    runs the fused epilogue (deterministic: fixed summation order).
-//  * gemm_tiled   -- M > 64 (prefill / large microbatches).  128x128x64 block
+//  * gemm_tiled   -- larger M (prefill, vocab projection).  128x128x64 block
 //    tile, 4 waves of 64x64, operands staged HBM -> LDS with 16-byte
 //    global_load_lds (LDS-DMA), XOR-swizzled on the source address so the
 //    ds_read_b128 fragment reads are bank-conflict free, double buffered,
 //    XCD-aware tile order.
+//  * gemm_ring    -- the tiled kernel's grids of <= 256 workgroups (decode
+//    microbatches of 65-256 rows): 128x64 (or 128x128) tiles, a 3-slot LDS
+//    ring with two k-steps in flight, 1 block/CU.
+//  * gemm_big     -- large prefill GEMMs: 256x256 tiles, 8 waves, 4-slot ring.
 //
 // Epilogues (fused, no extra pass): bias, gelu_new, silu(gate)*up, fp32
 // store, residual add into the fp32 residual stream, split-K slab, and the
@@ -630,16 +634,19 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles
   tiled_epilogue<EPI>(p, acc, smem, m0, n0, split, wm, wn, r, g);
 }
 
-// Ring variant of the 128x128 kernel (decode-sized M, few tiles): the
+// Ring variant of the tiled kernel (decode-sized M, few tiles): the
 // two-buffer loop above drains every LDS-DMA at each __syncthreads, so one
 // k-step of MFMAs (~512 cycles) is all that covers a load's latency.  Here a
 // ring of SLOTS k-steps keeps SLOTS-1 in flight while step kt computes:
-// counted `s_waitcnt vmcnt` retires only this thread's step-kt loads (8 glds
-// per step: 4 A + 4 W), one raw s_barrier per step publishes them AND proves
-// every wave finished step kt-1, whose slot is then refilled (guide §5
-// "Pipelining across barriers").  32 KiB per slot: 96 / 128 KiB, 1 block/CU,
-// which the under-filled decode grids do not miss.  Measured at 256 rows
-// (tools/microbench.py tiled3): QKV 26.1 -> 20.8 us, MLP-up 30.0 -> 24.1 us.
+// counted `s_waitcnt vmcnt` retires only this thread's step-kt loads (LPS glds
+// per step: 4 A + TN/32 W), one raw s_barrier per step publishes them AND
+// proves every wave finished step kt-1, whose slot is then refilled (guide §5
+// "Pipelining across barriers").  Tiles are 128 x TN (TN = 128, or 64: twice
+// the workgroups on the under-filled decode grids; 4 waves of 64 x TN/2).
+// 3 slots of 24 KiB (TN = 64) / 32 KiB (TN = 128).  Measured at 256 rows
+// (tools/microbench.py tiled3, GPT-2 XL): QKV 25.8 (double buffer) -> 20.5
+// (ring, 128 x 128) -> 15.6 us (ring, 128 x 64); MLP-up 29.4 -> 23.5 -> 17.3 us;
+// split-K decode kernel 23.3 / 26.2 us, hipBLASLt 19.3 / 20.0 us.
 template <int SLOTS, int TN>
 constexpr int smem_ring() {
   return TBM * (TN + 4) * 4 > SLOTS * (TILE_BYTES + TN * TBK * 2) ? TBM * (TN + 4) * 4
