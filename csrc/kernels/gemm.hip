@@ -1020,9 +1020,12 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
   }
   const int tn = (p.N + TBN - 1) / TBN;
   dim3 grid(tm * tn * p.splits), block(256);
-  if (tm * tn * p.splits <= g_tiled3_max_blocks && g_ring_slots == 4)
+  // the cap counts 128x64 tiles: a 128x128 ring grid gets half as many
+  // workgroups (vocab-wide lm_head grids stay on the 2-blocks/CU kernel)
+  const int cap128 = g_ring_tn == 64 ? g_tiled3_max_blocks / 2 : g_tiled3_max_blocks;
+  if (tm * tn * p.splits <= cap128 && g_ring_slots == 4)
     hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 128>), grid, block, 0, st, p, tm, tn);
-  else if (tm * tn * p.splits <= g_tiled3_max_blocks)
+  else if (tm * tn * p.splits <= cap128)
     hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 128>), grid, block, 0, st, p, tm, tn);
   else
     hipLaunchKernelGGL((gemm_tiled_kernel<EPI>), grid, block, 0, st, p, tm, tn);

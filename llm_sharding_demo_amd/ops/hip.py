@@ -103,7 +103,11 @@ class HipBackend(Backend):
     # 256 rows and 128x128 tiles QKV 25.8 -> 20.4 us, MLP-up 29.6 -> 23.3;
     # lm_head's 393-tile grid at 128 rows is better on the 2-blocks/CU kernel
     # (45.2 vs 47.7 us); 4 slots = 3 slots (profiles/r1_ab_ring_n64.log)
-    TILED3_MAX = int(os.environ.get("LSD_TILED3_MAX", "256"))
+    # Counted in 128x64 tiles (a 128x128 ring grid may use half).  512:
+    # Llama-3 8B's 28672-wide gate/up at 128 rows (448 tiles of 128x64) joins
+    # the ring, 18.6k -> 18.9k tok/s; residual splits keep their own 256
+    # target (RING_RESID_TARGET: GPT-2 XL loses 7 % with 512-WG slabs)
+    TILED3_MAX = int(os.environ.get("LSD_TILED3_MAX", "512"))
     RING_SLOTS = int(os.environ.get("LSD_RING_SLOTS", "3"))  # 3 or 4 (128 KiB of LDS)
     # ring tile columns, 128 or 64.  128x64 tiles double the workgroups of the
     # decode-sized grids: at 256 rows QKV 20.5 -> 15.6 us, MLP-up 23.5 -> 17.3
@@ -119,7 +123,7 @@ class HipBackend(Backend):
     #   Llama-3 8B 2 x 128: split-K 17.0k; >= 4800 wide 18.0-18.2k; all (N >= 4096) 18.7k
     TILED_ALL_M = int(os.environ.get("LSD_TILED_ALL_M", "128"))
     # workgroup target of split-K residual GEMMs on the ring (0 = TILED3_MAX)
-    RING_RESID_TARGET = int(os.environ.get("LSD_RING_RESID_TARGET", "0"))
+    RING_RESID_TARGET = int(os.environ.get("LSD_RING_RESID_TARGET", "256"))
     TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
     TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4000"))
 
