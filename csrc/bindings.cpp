@@ -14,6 +14,7 @@
 
 typedef lsd_bf16_t bf16;
 using lsd::GemmParams;
+using lsd::GemvParams;
 
 extern "C" {
 hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws, hipStream_t st);
@@ -40,6 +41,8 @@ hipError_t lsd_attn_prefill(const bf16* q, long ldq, const bf16* kc, const bf16*
                             const int* tiles, int n_tiles, const int* seq_slots,
                             const int* q_start, const int* cu_q, bf16* out, long ldo, int nh,
                             int n_kv, int hd, int max_seq, float scale_log2, hipStream_t st);
+int lsd_gemv_ok(int M, int K, int epi, int norm);
+hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st);
 hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                       const int* topk, const int* greedy, const long long* seeds,
                       const long long* step, int* out, hipStream_t st);
@@ -232,6 +235,104 @@ torch::Tensor linear_qkv(torch::Tensor a, torch::Tensor w, c10::optional<torch::
   return q;
 }
 
+// Small-M GEMV (csrc/kernels/gemv.hip): out = epi(norm?(x) @ w^T + bias).
+//   norm 0: x bf16 [M, K];  norm 1 (LayerNorm) / 2 (RMSNorm): x is the fp32
+//   residual [M, K], normalised in the kernel with gamma (+ beta).
+//   epi: 0 bf16, 1 gelu, 2 silu(gate)*up, 3 f32, 4 residual add into `resid`,
+//   6 QKV (q returned, k/v appended to the caches, optional RoPE).
+c10::optional<torch::Tensor> gemv(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias,
+                                  int64_t epi, int64_t norm, c10::optional<torch::Tensor> gamma,
+                                  c10::optional<torch::Tensor> beta, double eps,
+                                  c10::optional<torch::Tensor> resid,
+                                  c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
+                                  c10::optional<torch::Tensor> tslot, c10::optional<torch::Tensor> tpos,
+                                  int64_t q_size, int64_t kv_size, int64_t hd,
+                                  c10::optional<torch::Tensor> rope) {
+  need(w, torch::kBFloat16, "w");
+  need_rows(w, "w");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D with unit last stride");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "x must be 16-byte aligned");
+  GemvParams p{};
+  p.M = x.size(0); p.K = x.size(1); p.N = w.size(0);
+  TORCH_CHECK(w.size(1) == p.K, "K mismatch: x ", x.sizes(), " w ", w.sizes());
+  TORCH_CHECK(lsd_gemv_ok(p.M, p.K, (int)epi, (int)norm), "gemv: shape M=", p.M, " K=", p.K,
+              " epi=", epi, " norm=", norm, " not supported");
+  p.W = bptr(w); p.ldw = w.stride(0);
+  if (norm == 0) {
+    need(x, torch::kBFloat16, "x");
+    TORCH_CHECK(x.stride(0) % 8 == 0, "x row stride must be a multiple of 8");
+    p.A = bptr(x); p.lda = x.stride(0);
+  } else {
+    need(x, torch::kFloat32, "x");
+    TORCH_CHECK(x.stride(0) % 4 == 0 && p.K % 4 == 0, "x rows must be 16-byte aligned");
+    p.X = x.data_ptr<float>(); p.ldx = x.stride(0);
+    TORCH_CHECK(gamma.has_value(), "norm needs gamma");
+    need(*gamma, torch::kBFloat16, "gamma");
+    TORCH_CHECK(gamma->is_contiguous() && gamma->numel() == p.K, "gamma [K]");
+    p.gamma = bptr(*gamma);
+    if (norm == 1) {
+      TORCH_CHECK(beta.has_value(), "layernorm needs beta");
+      need(*beta, torch::kBFloat16, "beta");
+      TORCH_CHECK(beta->is_contiguous() && beta->numel() == p.K, "beta [K]");
+      p.beta = bptr(*beta);
+    }
+    p.eps = (float)eps;
+  }
+  if (bias.has_value()) {
+    need(*bias, torch::kBFloat16, "bias");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == p.N, "bias must be contiguous [N]");
+    p.bias = bptr(*bias);
+  }
+  c10::optional<torch::Tensor> ret;
+  auto bopt = w.options();
+  if (epi == EPI_RESID) {
+    TORCH_CHECK(resid.has_value(), "residual epilogue needs the residual");
+    need(*resid, torch::kFloat32, "resid");
+    TORCH_CHECK(resid->dim() == 2 && resid->is_contiguous() && resid->size(0) == p.M &&
+                resid->size(1) == p.N, "residual must be contiguous [M, N]");
+    p.out = resid->data_ptr(); p.ldo = p.N;
+  } else if (epi == EPI_F32) {
+    ret = torch::empty({p.M, p.N}, bopt.dtype(torch::kFloat32));
+    p.out = ret->data_ptr(); p.ldo = p.N;
+  } else if (epi == EPI_BF16 || epi == EPI_GELU) {
+    ret = torch::empty({p.M, p.N}, bopt);
+    p.out = ret->data_ptr(); p.ldo = p.N;
+  } else if (epi == EPI_SILU_MUL) {
+    TORCH_CHECK(p.N % 32 == 0 && !bias.has_value(), "silu_mul needs N % 32 == 0 and no bias");
+    ret = torch::empty({p.M, p.N / 2}, bopt);
+    p.out = ret->data_ptr(); p.ldo = p.N / 2;
+  } else if (epi == EPI_QKV) {
+    TORCH_CHECK(kc.has_value() && vc.has_value() && tslot.has_value() && tpos.has_value(),
+                "qkv needs caches and token slots/positions");
+    need(*kc, torch::kBFloat16, "k_cache");
+    need(*vc, torch::kBFloat16, "v_cache");
+    TORCH_CHECK(kc->dim() == 4 && kc->is_contiguous() && vc->sizes() == kc->sizes() && vc->is_contiguous(),
+                "caches must be contiguous [slots, n_kv, max_seq, hd]");
+    TORCH_CHECK(kc->size(3) == hd && kc->size(1) * hd == kv_size, "cache shape mismatch");
+    TORCH_CHECK(p.N == q_size + 2 * kv_size && q_size % hd == 0 && hd % 2 == 0, "bad qkv dims");
+    need(*tslot, torch::kInt32, "token_slots");
+    need(*tpos, torch::kInt32, "token_pos");
+    TORCH_CHECK(tslot->numel() == p.M && tpos->numel() == p.M && tslot->is_contiguous() &&
+                tpos->is_contiguous(), "token_slots/token_pos must be contiguous [M]");
+    p.kc = bptr_mut(*kc); p.vc = bptr_mut(*vc);
+    p.tslot = tslot->data_ptr<int>(); p.tpos = tpos->data_ptr<int>();
+    p.q_size = q_size; p.kv_size = kv_size; p.hd = hd;
+    p.max_seq = kc->size(2); p.n_kv = kc->size(1);
+    if (rope.has_value()) {
+      need(*rope, torch::kFloat32, "rope");
+      TORCH_CHECK(rope->is_contiguous() && rope->dim() == 3 && rope->size(1) == hd / 2 &&
+                  rope->size(2) == 2 && rope->size(0) >= p.max_seq, "rope table must be [>=max_seq, hd/2, 2]");
+      p.rope = rope->data_ptr<float>();
+    }
+    ret = torch::empty({p.M, q_size}, bopt);
+    p.out = ret->data_ptr(); p.ldo = q_size;
+  } else {
+    TORCH_CHECK(false, "gemv: unknown epilogue ", epi);
+  }
+  check_hip(lsd_gemv(&p, (int)epi, (int)norm, cur_stream()), "gemv");
+  return ret;
+}
+
 torch::Tensor embed(torch::Tensor ids, torch::Tensor pos, torch::Tensor wte,
                     c10::optional<torch::Tensor> wpe) {
   need(ids, torch::kInt32, "ids");
@@ -407,6 +508,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_decode", &attn_decode);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample);
+  m.def("gemv", &gemv);
+  m.def("gemv_ok", [](int64_t M, int64_t K, int64_t epi, int64_t norm) {
+    return lsd_gemv_ok((int)M, (int)K, (int)epi, (int)norm) != 0; });
   m.def("set_stamps", &set_stamps);
   // tiled GEMMs with >= this many 256x256 tiles use the pipelined 256^2 kernel
   m.def("gemm_set_big_min", [](int64_t v) { lsd_gemm_set_big_min((int)v); });

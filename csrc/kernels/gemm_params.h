@@ -25,4 +25,23 @@ struct GemmParams {
   long long* stamps;  // diagnostic builds only: per-workgroup s_memrealtime phase stamps
 };
 
+// Small-M (M <= 8) weight-streaming GEMV with an optional fused input norm
+// (csrc/kernels/gemv.hip).  Epilogue codes are the GemmParams ones.
+struct GemvParams {
+  const lsd_bf16_t* A; long lda;      // bf16 input rows [M][K] (norm == 0)
+  const float* X; long ldx;           // fp32 residual rows [M][K] (norm != 0)
+  const lsd_bf16_t* gamma;            // norm weight [K]
+  const lsd_bf16_t* beta;             // LayerNorm bias [K] (null: RMSNorm)
+  float eps;
+  const lsd_bf16_t* W; long ldw;      // [N][K]
+  int M, N, K;
+  const lsd_bf16_t* bias;             // [N] or null
+  void* out; long ldo;                // bf16 / f32 out, or the fp32 residual (EPI_RESID)
+  // QKV epilogue (same meaning as GemmParams)
+  lsd_bf16_t* kc; lsd_bf16_t* vc;
+  const int* tslot; const int* tpos;
+  int q_size, kv_size, hd, max_seq, n_kv;
+  const float* rope;
+};
+
 }  // namespace lsd

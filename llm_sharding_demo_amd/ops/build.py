@@ -27,7 +27,7 @@ BUILD = os.path.join(ROOT, "build", "native")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-KERNELS = ["gemm.hip", "norm.hip", "attention.hip", "sample.hip"]
+KERNELS = ["gemm.hip", "gemv.hip", "norm.hip", "attention.hip", "sample.hip"]
 EXT_NAME = "_C"
 
 

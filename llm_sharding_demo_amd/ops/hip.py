@@ -78,8 +78,38 @@ def prefill_tiles(meta) -> torch.Tensor:
     return torch.tensor(tiles, dtype=torch.int32).reshape(-1, 2)
 
 
+class LazyNorm:
+    """A norm whose output has not been materialised: at M <= GEMV_NORM_MAX_M
+    rows the consuming GEMV (csrc/kernels/gemv.hip) normalises the fp32
+    residual rows itself, so the separate norm launch disappears.  Any other
+    consumer materialises it through the norm kernel."""
+
+    __slots__ = ("x", "w", "b", "eps", "rms")
+
+    def __init__(self, x, w, b, eps, rms):
+        self.x, self.w, self.b, self.eps, self.rms = x, w, b, eps, rms
+
+    @property
+    def shape(self):
+        return self.x.shape
+
+    @property
+    def code(self) -> int:  # gemv norm code: 1 LayerNorm, 2 RMSNorm
+        return 2 if self.rms else 1
+
+
+# gemv epilogue codes (csrc/kernels/gemm.hip Epi)
+_EPI = {"none": 0, "gelu": 1, "silu_mul": 2}
+EPI_F32, EPI_RESID, EPI_QKV = 3, 4, 6
+
+
 class HipBackend(Backend):
     name = "hip"
+    # Decode GEMMs of at most GEMV_MAX_M rows run on the weight-streaming GEMV
+    # (no split-K, fused epilogues); at most GEMV_NORM_MAX_M rows it also folds
+    # the preceding LayerNorm / RMSNorm into its prologue.  0 disables.
+    GEMV_MAX_M = int(os.environ.get("LSD_GEMV_MAX_M", "8"))
+    GEMV_NORM_MAX_M = int(os.environ.get("LSD_GEMV_NORM_MAX_M", "2"))
     TARGET_BLOCKS = 512  # >> 256 CUs so every CU streams
     # decode GEMM: aim for this many workgroups (column tiles x k-splits)
     # decode (split-K, last-arriver) GEMM up to this many rows (above 128 as
@@ -215,6 +245,8 @@ class HipBackend(Backend):
         return self.C.embed(ids, pos, wte, wpe)
 
     def _norm(self, r: Residual, w, b, eps, rms: bool):
+        if not r.pending and r.x.shape[0] <= self.GEMV_NORM_MAX_M and r.x.shape[1] % 8 == 0:
+            return LazyNorm(r.x, w, b, eps, rms)
         self._flush_extra(r)
         slab, pb = (r.pending[0] if r.pending else (None, None))
         out = self.C.norm(r.x, slab, pb, w, b, eps, rms, None, True)
@@ -239,9 +271,37 @@ class HipBackend(Backend):
         return self._norm(r, w, None, eps, True)
 
     def norm_rows(self, x, w, b, eps, rms: bool, rows=None):
+        if rows is None and x.shape[0] <= self.GEMV_NORM_MAX_M and x.shape[1] % 8 == 0:
+            return LazyNorm(x, w, b, eps, rms)
         return self.C.norm(x, None, None, w, b, eps, rms, rows, True)
 
+    def materialize(self, xn):
+        if isinstance(xn, LazyNorm):
+            return self.C.norm(xn.x, None, None, xn.w, xn.b, xn.eps, xn.rms, None, True)
+        return xn
+
+    def _gemv_in(self, xn, K: int, epi: int):
+        """(x, norm code, gamma, beta, eps) for a GEMV launch, or None when this
+        GEMM does not run on the GEMV (the caller takes the MFMA path)."""
+        M = xn.shape[0]
+        if M > self.GEMV_MAX_M:
+            return None
+        if isinstance(xn, LazyNorm):
+            if self.C.gemv_ok(M, K, epi, xn.code):
+                return xn.x, xn.code, xn.w, xn.b, xn.eps
+            xn = self.materialize(xn)
+        if self.C.gemv_ok(M, K, epi, 0):
+            return xn, 0, None, None, 0.0
+        return None
+
     def qkv_kv_append(self, xn, w, b, cache_k, cache_v, meta, mcfg):
+        g = self._gemv_in(xn, w.shape[1], EPI_QKV)
+        if g is not None:
+            x, nc, gw, gb, eps = g
+            return self.C.gemv(x, w, b, EPI_QKV, nc, gw, gb, eps, None, cache_k, cache_v,
+                               meta.token_slots, meta.token_pos, mcfg.q_size, mcfg.kv_size,
+                               mcfg.head_dim, self._rope)
+        xn = self.materialize(xn)
         tiled, splits = self._gemm_kw(xn.shape[0], w.shape[0], w.shape[1])
         return self.C.linear_qkv(xn, w, b, cache_k, cache_v, meta.token_slots, meta.token_pos,
                                  mcfg.q_size, mcfg.kv_size, mcfg.head_dim, self._rope,
@@ -264,13 +324,23 @@ class HipBackend(Backend):
                                    meta.cu_q, nh)
 
     def linear(self, a, w, b=None, act: str = "none"):
-        code = {"none": 0, "gelu": 1, "silu_mul": 2}[act]
+        code = _EPI[act]
+        g = self._gemv_in(a, w.shape[1], code)
+        if g is not None:
+            x, nc, gw, gb, eps = g
+            return self.C.gemv(x, w, b, code, nc, gw, gb, eps, None, None, None, None, None,
+                               0, 0, 0, None)
+        a = self.materialize(a)
         tiled, splits = self._gemm_kw(a.shape[0], w.shape[0], w.shape[1], 2 if code == 2 else 1)
         return self.C.linear(a, w, b, code, tiled, splits, self.counters)
 
     def linear_residual(self, a, w, b, r: Residual) -> None:
         M, K = a.shape
         N = w.shape[0]
+        if self._gemv_in(a, K, EPI_RESID) is not None:  # adds straight into r.x
+            self.C.gemv(a, w, b, EPI_RESID, 0, None, None, 0.0, r.x, None, None, None, None,
+                        0, 0, 0, None)
+            return
         splits = self._resid_splits(M, N, K)
         tiled = self._tiled(M, N)
         # decode split-K: hand the S partial slabs to the next norm (which
@@ -281,6 +351,12 @@ class HipBackend(Backend):
             r.pending.append((slab, b))
 
     def logits(self, xn, w):
+        g = self._gemv_in(xn, w.shape[1], EPI_F32)
+        if g is not None:
+            x, nc, gw, gb, eps = g
+            return self.C.gemv(x, w, None, EPI_F32, nc, gw, gb, eps, None, None, None, None,
+                               None, 0, 0, 0, None)
+        xn = self.materialize(xn)
         # vocab-wide N: the 128x128 LDS-tiled kernel fills the chip without
         # split-K and reads the activation rows once per 128 columns instead
         # of once per 64 -- measured 41.8 vs 64.2 us at M = 128 (GPT-2 XL),
