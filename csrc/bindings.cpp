@@ -23,6 +23,7 @@ void lsd_gemm_set_tiled3_max(int v);
 void lsd_gemm_set_ring_slots(int v);
 void lsd_gemm_set_ring_tn(int v);
 void lsd_attn_set_max_wg(int v);
+void lsd_attn_set_small_waves(int v);
 int lsd_gemm_sk_rows(int M, int N, int S);
 int lsd_gemm_sk_rblocks(int M, int N, int S);
 int lsd_gemm_sk_nw(int M, int epi);
@@ -42,6 +43,7 @@ hipError_t lsd_attn_prefill(const bf16* q, long ldq, const bf16* kc, const bf16*
                             const int* q_start, const int* cu_q, bf16* out, long ldo, int nh,
                             int n_kv, int hd, int max_seq, float scale_log2, hipStream_t st);
 int lsd_gemv_ok(int M, int K, int epi, int norm);
+void lsd_gemv_set_nt(int v);
 hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st);
 hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                       const int* topk, const int* greedy, const long long* seeds,
@@ -509,6 +511,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample);
   m.def("gemv", &gemv);
+  // GEMV weight stream with non-temporal loads (A/B knob, LSD_GEMV_NT)
+  m.def("gemv_set_nt", [](int64_t v) { lsd_gemv_set_nt((int)v); });
   m.def("gemv_ok", [](int64_t M, int64_t K, int64_t epi, int64_t norm) {
     return lsd_gemv_ok((int)M, (int)K, (int)epi, (int)norm) != 0; });
   m.def("set_stamps", &set_stamps);
@@ -519,6 +523,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_ring_tn", [](int64_t v) { lsd_gemm_set_ring_tn((int)v); });
   // decode attention: cap the grid (blocks loop over (sequence, head) items)
   m.def("attn_set_max_wg", [](int64_t v) { lsd_attn_set_max_wg((int)v); });
+  // decode attention: waves per block when the batch has few (sequence, head) items
+  m.def("attn_set_small_waves", [](int64_t v) { lsd_attn_set_small_waves((int)v); });
   // decode GEMM: rows per row block (M above it runs as several row blocks)
   m.def("gemm_set_sk_rows", [](int64_t v) { lsd_gemm_set_sk_rows((int)v); });
   m.def("gemm_sk_rblocks", [](int64_t M, int64_t N, int64_t S) { return lsd_gemm_sk_rblocks((int)M, (int)N, (int)S); });

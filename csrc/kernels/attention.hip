@@ -37,15 +37,18 @@ constexpr float NEG = -1e30f;
 #define LSD_KV_LOAD ld8_nt
 #endif
 
-template <int HD, int G, int U>
-__global__ __launch_bounds__(256) void attn_decode_kernel(
+// NWV waves per block: 4 for full batches; 16 for small ones (fewer
+// (sequence, head) items than CUs), where the whole context of an item is
+// requested in one round of loads instead of a chain of dependent rounds.
+template <int HD, int G, int U, int NWV>
+__global__ __launch_bounds__(NWV * 64) void attn_decode_kernel(
     const bf16* __restrict__ q, long ldq, const bf16* __restrict__ kc,
     const bf16* __restrict__ vc, const int* __restrict__ seq_slots,
     const int* __restrict__ qpos, bf16* out, long ldo, float* part_o, float* part_ml, int n_kv,
     int max_seq, int splits, float scale_log2, int n_items) {
   constexpr int LPK = HD / 8;    // lanes per key row
   constexpr int KPI = 64 / LPK;  // keys per wave-instruction
-  __shared__ float sm[4][G][LPK][10];
+  __shared__ float sm[NWV][G][LPK][10];
   // work item = (sequence, kv head); a capped grid (lsd_attn_set_max_wg) loops
   // over items so the kernel occupies only part of the chip and a concurrent
   // lane's GEMMs keep the rest
@@ -74,14 +77,22 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
     }
 
-    for (int c0 = k_lo + w * KPI; c0 < k_hi; c0 += 4 * KPI * U) {
-      bf16x8 kv[U];
+    for (int c0 = k_lo + w * KPI; c0 < k_hi; c0 += NWV * KPI * U) {
+      bf16x8 kv[U], vv[U];
       int key[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        key[u] = c0 + u * 4 * KPI + kg;
+        key[u] = c0 + u * NWV * KPI + kg;
         const int kk = min(key[u], k_hi - 1);
         kv[u] = LSD_KV_LOAD(kc + base + (long)kk * HD);
+      }
+      // small batches: V (independent of the scores) is requested with K, one
+      // round trip per item.  Full batches keep V behind the scores: fewer
+      // live registers, and the other blocks on the CU hide the latency
+      // (measured: moving it costs the 2 x 256 bench ~1.5 %)
+      if constexpr (NWV > 4) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) vv[u] = LSD_KV_LOAD(vc + base + (long)min(key[u], k_hi - 1) * HD);
       }
       float s[G][U];
 #pragma unroll
@@ -92,12 +103,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc += qf[g][j] * bf2f(kv[u][j]);
 #pragma unroll
-          for (int msk = 1; msk < LPK; msk <<= 1) acc += shfl_xor(acc, msk);
+          for (int msk = 1; msk < LPK; msk <<= 1) acc += wave_xchg_n(acc, msk);
           s[g][u] = key[u] < k_hi ? acc : NEG;
         }
-      bf16x8 vv[U];
+      if constexpr (NWV <= 4) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) vv[u] = LSD_KV_LOAD(vc + base + (long)min(key[u], k_hi - 1) * HD);
+        for (int u = 0; u < U; ++u) vv[u] = LSD_KV_LOAD(vc + base + (long)min(key[u], k_hi - 1) * HD);
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float mx = s[g][0];
@@ -128,12 +140,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     for (int msk = LPK; msk < 64; msk <<= 1) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const float mo = shfl_xor(m[g], msk), lo = shfl_xor(l[g], msk);
+        // lanes of one head-dim slice (equal ds) merge: exact xor partners
+        const float mo = wave_xor_n(m[g], msk), lo = wave_xor_n(l[g], msk);
         const float mn = fmaxf(m[g], mo);
         const float a = exp2f(m[g] - mn), bb = exp2f(mo - mn);
         l[g] = l[g] * a + lo * bb;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + shfl_xor(o[g][j], msk) * bb;
+        for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + wave_xor_n(o[g][j], msk) * bb;
         m[g] = mn;
       }
     }
@@ -153,10 +166,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       for (int g = 0; g < G; ++g) {
         float mm = NEG;
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) mm = fmaxf(mm, sm[ww][g][ds][0]);
+        for (int ww = 0; ww < NWV; ++ww) mm = fmaxf(mm, sm[ww][g][ds][0]);
         float ll = 0.f, oo[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) {
+        for (int ww = 0; ww < NWV; ++ww) {
           const float f = exp2f(sm[ww][g][ds][0] - mm);
           ll += sm[ww][g][ds][1] * f;
 #pragma unroll
@@ -298,8 +311,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
         sacc[ni][i] = sv;
         tmax = fmaxf(tmax, sv);
       }
-    tmax = fmaxf(tmax, shfl_xor(tmax, 16));
-    tmax = fmaxf(tmax, shfl_xor(tmax, 32));
+    tmax = fmaxf(tmax, wave_xchg<16>(tmax));
+    tmax = fmaxf(tmax, wave_xchg<32>(tmax));
     const float mn = fmaxf(m, tmax);
     const float alpha = exp2f(m - mn);
     m = mn;
@@ -337,8 +350,8 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
     }
     __syncthreads();
   }
-  lsum += shfl_xor(lsum, 16);
-  lsum += shfl_xor(lsum, 32);
+  lsum += wave_xchg<16>(lsum);
+  lsum += wave_xchg<32>(lsum);
   if (qi < qlen) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16* op = out + (long)qrow * ldo + (long)h * HD;
@@ -358,6 +371,8 @@ using namespace lsd;
 
 static int g_attn_max_wg = 0;  // 0: one workgroup per (sequence, kv head)
 extern "C" void lsd_attn_set_max_wg(int v) { g_attn_max_wg = v; }
+static int g_attn_small_waves = 8;  // waves per block for small decode batches (4, 8, 16)
+extern "C" void lsd_attn_set_small_waves(int v) { g_attn_small_waves = v; }
 
 extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
                                       const int* seq_slots, const int* qpos, bf16* out, long ldo,
@@ -368,13 +383,25 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
   const int G = nh / n_kv;
   const int n_items = B * n_kv;
   const int gx = g_attn_max_wg > 0 ? (n_items < g_attn_max_wg ? n_items : g_attn_max_wg) : n_items;
-  dim3 grid(gx, splits), block(256);
-#define LSD_DEC(HDV, GV)                                                                      \
-  if (hd == HDV && G == GV) {                                                                 \
-    hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 4>), grid, block, 0, st, q, ldq, kc, vc,  \
-                       seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq, splits,     \
-                       scale_log2, n_items);                                                  \
-    goto combine;                                                                             \
+  // fewer blocks than half the CUs: wider blocks (g_attn_small_waves waves),
+  // K and V of an item requested in one round of loads
+  const int sw = (long)gx * splits <= 128 ? g_attn_small_waves : 0;
+  dim3 grid(gx, splits);
+#define LSD_DEC(HDV, GV)                                                                        \
+  if (hd == HDV && G == GV) {                                                                   \
+    if (sw == 16)                                                                               \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 2, 16>), grid, dim3(1024), 0, st, q, ldq, \
+                         kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq,     \
+                         splits, scale_log2, n_items);                                          \
+    else if (sw == 8)                                                                           \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 4, 8>), grid, dim3(512), 0, st, q, ldq,   \
+                         kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq,     \
+                         splits, scale_log2, n_items);                                          \
+    else                                                                                        \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 4, 4>), grid, dim3(256), 0, st, q, ldq,   \
+                         kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq,     \
+                         splits, scale_log2, n_items);                                          \
+    goto combine;                                                                               \
   }
   LSD_DEC(64, 1)
   LSD_DEC(64, 2)

@@ -56,9 +56,64 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 template <typename T>
 __device__ __forceinline__ T shfl_xor(T v, int m) { return __shfl_xor(v, m, 64); }
 
+// Partner exchange across lane bit log2(OFF) without the LDS crossbar
+// (ds_bpermute costs an LDS round trip per step): DPP quad permutes for
+// OFF = 1, 2; row half-mirror / mirror (lane i <-> 7-i / 15-i) for 4, 8;
+// v_permlane16/32_swap for 16, 32.  Each is an involution that pairs lanes
+// differing in that bit, which is all a butterfly reduction needs; the
+// partner is lane ^ OFF except for OFF = 4, 8 (mirror order).
+template <int OFF>
+__device__ __forceinline__ float wave_xchg(float v) {
+  const int x = __builtin_bit_cast(int, v);
+  if constexpr (OFF == 1) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));
+  } else if constexpr (OFF == 2) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));
+  } else if constexpr (OFF == 4) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false));
+  } else if constexpr (OFF == 8) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false));
+  } else if constexpr (OFF == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return __builtin_bit_cast(float, (threadIdx.x & 16) ? (int)r[0] : (int)r[1]);
+  } else {
+    static_assert(OFF == 32, "offset must be a power of two <= 32");
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return __builtin_bit_cast(float, (threadIdx.x & 32) ? (int)r[0] : (int)r[1]);
+  }
+}
+
+// wave_xchg with an offset that is a compile-time constant after unrolling
+__device__ __forceinline__ float wave_xchg_n(float v, int off) {
+  switch (off) {
+    case 1: return wave_xchg<1>(v);
+    case 2: return wave_xchg<2>(v);
+    case 4: return wave_xchg<4>(v);
+    case 8: return wave_xchg<8>(v);
+    case 16: return wave_xchg<16>(v);
+    default: return wave_xchg<32>(v);
+  }
+}
+
+// Exact lane ^ off partner (values of non-equivalent lanes, e.g. merging
+// per-dimension partials): mirrors replaced by ds_bpermute for 4 and 8.
+__device__ __forceinline__ float wave_xor_n(float v, int off) {
+  switch (off) {
+    case 1: return wave_xchg<1>(v);
+    case 2: return wave_xchg<2>(v);
+    case 16: return wave_xchg<16>(v);
+    case 32: return wave_xchg<32>(v);
+    default: return shfl_xor(v, off);
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += shfl_xor(v, m);
+  v += wave_xchg<1>(v);
+  v += wave_xchg<2>(v);
+  v += wave_xchg<4>(v);
+  v += wave_xchg<8>(v);
+  v += wave_xchg<16>(v);
+  v += wave_xchg<32>(v);
   return v;
 }
 __device__ __forceinline__ float wave_max(float v) {

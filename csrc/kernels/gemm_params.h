@@ -42,6 +42,7 @@ struct GemvParams {
   const int* tslot; const int* tpos;
   int q_size, kv_size, hd, max_seq, n_kv;
   const float* rope;
+  int nt;                             // 1: stream W with non-temporal loads
 };
 
 }  // namespace lsd

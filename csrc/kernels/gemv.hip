@@ -62,6 +62,26 @@ __device__ __forceinline__ int gv_row(int gw, int j) {
   }
 }
 
+// One butterfly step at lane bit OFF over the first N live values: lanes with
+// the bit set keep the upper half, the others the lower half, each adding
+// the partner's copy of the half it keeps (N == 1: plain pairwise sum).
+template <int OFF, int N, int V>
+__device__ __forceinline__ void gv_step(float (&acc)[V], int& idx, int lane) {
+  if constexpr (N == 1) {
+    acc[0] += wave_xchg<OFF>(acc[0]);
+  } else {
+    constexpr int h = N / 2;
+    const bool up = (lane & OFF) != 0;
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      const float send = up ? acc[i] : acc[i + h];
+      const float keep = up ? acc[i + h] : acc[i];
+      acc[i] = keep + wave_xchg<OFF>(send);
+    }
+    if (up) idx += h;
+  }
+}
+
 // Block-wide sums of MR values at once (one LDS round for all rows).
 template <int MR>
 __device__ __forceinline__ void block_sums(float (&v)[MR], float* red) {
@@ -126,12 +146,21 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
 
     // ---- 2. the weight stream: every chunk of this wave's rows, issued now
     bf16x8 wv[CPW][SLOTS];
+    // waves past N re-read row N-1 (never stored)
+    if (p.nt) {  // wave-uniform: weights read once per token need not stay cached
 #pragma unroll
-    for (int j = 0; j < CPW; ++j) {
-      // waves past N re-read row N-1 (never stored)
-      const bf16* wr = p.W + (long)min(gv_row<EPI, CPW>(gw, j), p.N - 1) * p.ldw;
+      for (int j = 0; j < CPW; ++j) {
+        const bf16* wr = p.W + (long)min(gv_row<EPI, CPW>(gw, j), p.N - 1) * p.ldw;
 #pragma unroll
-      for (int i = 0; i < SLOTS; ++i) wv[j][i] = ld8(wr + min(lane + 64 * i, KC - 1) * 8);
+        for (int i = 0; i < SLOTS; ++i) wv[j][i] = ld8_nt(wr + min(lane + 64 * i, KC - 1) * 8);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < CPW; ++j) {
+        const bf16* wr = p.W + (long)min(gv_row<EPI, CPW>(gw, j), p.N - 1) * p.ldw;
+#pragma unroll
+        for (int i = 0; i < SLOTS; ++i) wv[j][i] = ld8(wr + min(lane + 64 * i, KC - 1) * 8);
+      }
     }
 
     // ---- 3. input prologue -> LDS (runs while the weights are in flight)
@@ -206,31 +235,16 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
       }
     }
 
-    // ---- 5. butterfly reduce-scatter over the wave: halving steps leave lane
-    // group g with the full sum of value idx(g); then plain xor steps
+    // ---- 5. butterfly reduce-scatter over the wave (DPP / permlane swaps):
+    // halving steps leave each lane group with the full sum of one value
+    // idx; the remaining steps are plain pairwise sums
     int idx = 0;
-    {
-      int n = V;
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        if (n > 1) {
-          const bool up = (lane & off) != 0;
-          const int h = n >> 1;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if (i < h) {
-              const float send = up ? acc[i] : acc[i + h];
-              const float keep = up ? acc[i + h] : acc[i];
-              acc[i] = keep + shfl_xor(send, off);
-            }
-          }
-          if (up) idx += h;
-          n = h;
-        } else {
-          acc[0] += shfl_xor(acc[0], off);
-        }
-      }
-    }
+    gv_step<32, V>(acc, idx, lane);
+    gv_step<16, (V > 1 ? V / 2 : 1)>(acc, idx, lane);
+    gv_step<8, (V > 2 ? V / 4 : 1)>(acc, idx, lane);
+    gv_step<4, (V > 4 ? V / 8 : 1)>(acc, idx, lane);
+    gv_step<2, (V > 8 ? V / 16 : 1)>(acc, idx, lane);
+    gv_step<1, 1>(acc, idx, lane);
     if ((lane & (64 / V - 1)) == 0) red[w * 16 + idx] = acc[0];
     __syncthreads();
 
@@ -322,8 +336,14 @@ extern "C" int lsd_gemv_ok(int M, int K, int epi, int norm) {
   return 1;
 }
 
-extern "C" hipError_t lsd_gemv(const GemvParams* p, int epi, int norm, hipStream_t st) {
-  if (!lsd_gemv_ok(p->M, p->K, epi, norm)) return hipErrorInvalidValue;
+static int g_gemv_nt = 0;
+extern "C" void lsd_gemv_set_nt(int v) { g_gemv_nt = v; }
+
+extern "C" hipError_t lsd_gemv(const GemvParams* pin, int epi, int norm, hipStream_t st) {
+  if (!lsd_gemv_ok(pin->M, pin->K, epi, norm)) return hipErrorInvalidValue;
+  GemvParams q = *pin;
+  q.nt = g_gemv_nt;
+  const GemvParams* p = &q;
   const int mr = gv_mr(p->M), nb = gv_nb(p->K);
   switch (epi * 4 + norm) {
     case gv::BF16 * 4 + gv::NONE: return gemv_launch<gv::BF16, gv::NONE>(*p, mr, nb, st);

@@ -165,6 +165,8 @@ class HipBackend(Backend):
         self.C.gemm_set_ring_slots(self.RING_SLOTS)
         self.C.gemm_set_ring_tn(self.RING_TN)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
+        self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
+        self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))
         self.counters = None
         self._rope = None
         self.lane = 0  # microbatch lane (stream) currently being issued; see pipeline.py

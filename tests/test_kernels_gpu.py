@@ -295,21 +295,30 @@ def test_qkv_kv_append(C, CNT, rope, mode):
 @pytest.mark.parametrize("hd,nh,n_kv", [(64, 4, 4), (64, 8, 2), (128, 8, 2), (128, 32, 8)])
 @pytest.mark.parametrize("splits", [1, 3])
 @pytest.mark.parametrize("max_wg", [0, 3])
-def test_attention_decode(C, hd, nh, n_kv, splits, max_wg):
-    """max_wg > 0: capped grid, each block loops over (sequence, head) items."""
+@pytest.mark.parametrize("B,small_waves", [(5, 8), (5, 16), (5, 4), (70, 8)])
+def test_attention_decode(C, hd, nh, n_kv, splits, max_wg, B, small_waves):
+    """max_wg > 0: capped grid, each block loops over (sequence, head) items.
+    B = 5: the small-batch blocks (8 / 16 / 4 waves); B = 70: 4-wave blocks."""
     C.attn_set_max_wg(max_wg)
+    C.attn_set_small_waves(small_waves)
     try:
-        _attention_decode_case(C, hd, nh, n_kv, splits)
+        _attention_decode_case(C, hd, nh, n_kv, splits, B)
     finally:
         C.attn_set_max_wg(0)
+        C.attn_set_small_waves(8)
 
 
-def _attention_decode_case(C, hd, nh, n_kv, splits):
-    B, slots, S = 5, 6, 300
+def _attention_decode_case(C, hd, nh, n_kv, splits, B=5):
+    slots, S = max(6, B), 300
     kc, vc = bf(slots, n_kv, S, hd, seed=16), bf(slots, n_kv, S, hd, seed=17)
     q = bf(B, nh * hd, seed=18)
-    seq_slots = torch.tensor([5, 0, 2, 3, 1], dtype=torch.int32, device=DEV)
-    pos = torch.tensor([0, 17, 63, 140, 299], dtype=torch.int32, device=DEV)
+    if B == 5:
+        seq_slots = torch.tensor([5, 0, 2, 3, 1], dtype=torch.int32, device=DEV)
+        pos = torch.tensor([0, 17, 63, 140, 299], dtype=torch.int32, device=DEV)
+    else:
+        g = torch.Generator().manual_seed(B)
+        seq_slots = torch.randperm(slots, generator=g)[:B].int().to(DEV)
+        pos = torch.randint(0, S, (B,), generator=g).int().to(DEV)
     o = C.attn_decode(q, kc, vc, seq_slots, pos, nh, splits)
     cu = torch.arange(B + 1, dtype=torch.int32)
     o_ref = ref.attention(q.reshape(B, nh, hd).cpu(), kc.cpu(), vc.cpu(), seq_slots.cpu(), pos.cpu(), cu)
