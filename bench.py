@@ -48,6 +48,9 @@ def parse():
                    help="pipeline replicas: N GPUs = (N/dp)-stage pipeline x dp (default 1: ppN)")
     p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),
                    help="nccl (RCCL over xGMI) | gloo (host-staged, for rehearsals)")
+    p.add_argument("--loopback-stages", type=int, default=0,
+                   help="rehearsal: run this many pipeline stages as threads on ONE GPU "
+                        "(device-async loopback transport); --batch is then the total batch")
     p.add_argument("--device", default="cuda",
                    help="cuda (MI355X); cpu only to rehearse the multi-rank contract with gloo")
     p.add_argument("--greedy", action="store_true")
@@ -71,30 +74,28 @@ def main() -> int:
     if N % R:
         raise SystemExit(f"--gpus {N} is not a multiple of --dp {R}")
     P = N // R                      # pipeline stages per replica
-    M = args.microbatches or 2 * P  # microbatches per replica
+    M = args.microbatches or 2 * P  # microbatch groups per replica
     B = N * args.batch              # global batch (weak scaling: fixed per GPU)
     Br = P * args.batch             # sequences per replica
+    transport = args.transport
+    if args.loopback_stages:
+        if N != 1:
+            raise SystemExit("--loopback-stages runs on one GPU")
+        P = args.loopback_stages
+        M = args.microbatches or 2 * P
+        transport = "loopback"
     cfg = EngineConfig(model_id=args.model, num_stages=P, dp_replicas=R, max_batch=Br,
                        max_seq_len=args.prompt + args.gen, device=args.device,
                        use_graphs=not args.no_graphs, num_microbatches=M, seed=args.seed,
-                       transport=args.transport)
+                       transport=transport)
     eng = Engine(cfg, mode="dist" if N > 1 else "local")
     rank = eng.rank
-    worker = eng.workers[0]
 
     vocab = cfg.model.vocab_size
     sp = SamplingParams(greedy=args.greedy, temperature=0.6, top_k=40,
                         max_new_tokens=args.gen, seed=1234)
-    # every rank builds the identical per-replica round specs (deterministic),
-    # no broadcast; each rank runs its own replica's
-    specs = []
-    for rep in range(R):
-        rnd = random.Random(args.seed * 1000 + rep)
-        prompts = [[rnd.randrange(vocab) for _ in range(args.prompt)] for _ in range(Br)]
-        eng._rng = random.Random(args.seed * 1000 + rep)
-        specs.append(eng.make_round(prompts, [sp] * Br, list(range(Br)), microbatches=M,
-                                    record_timing=(rank == 0)))
-    spec = specs[eng.replica]
+    rnd = random.Random(args.seed)
+    prompts = [[rnd.randrange(vocab) for _ in range(args.prompt)] for _ in range(B)]
 
     def barrier():
         if N > 1:
@@ -104,19 +105,28 @@ def main() -> int:
         if args.device != "cpu":
             torch.cuda.synchronize()
 
+    def session(timing: bool):
+        """One bench step = one generation session of the whole global batch:
+        every sequence joins at step 0 (prefill), decodes, and leaves."""
+        if rank == 0:
+            eng.generate_ids(prompts, [sp] * B, record_timing=timing)
+        else:
+            eng.follow_session()
+
     for _ in range(args.warmup):
-        worker.run_round(spec)
+        session(False)
     sync()
     barrier()
     sync()
     t0 = time.perf_counter()
     step_ms, prefill_ms, max_step = [], [], []
     for _ in range(args.steps):
-        res = worker.run_round(spec)
-        if rank == 0 and res is not None:
-            step_ms += res.step_times_ms
-            prefill_ms.append(res.prefill_ms)
-            max_step.append(max(res.step_times_ms, default=0.0))
+        session(True)
+        if rank == 0 and eng.last_session is not None:
+            ls = eng.last_session
+            step_ms += ls.step_times_ms
+            prefill_ms.append(ls.prefill_ms)
+            max_step.append(max(ls.step_times_ms, default=0.0))
     sync()
     barrier()
     sync()
@@ -143,18 +153,22 @@ def main() -> int:
             "data": "synthetic prompts, random-init weights",
             "p50_token_latency_ms": round(p50, 4) if p50 is not None else None,
             # stage-0 clock, mean per timed step: prefill (TTFT of the batch)
-            # and the slowest decode step (hipGraph capture happens in one)
+            # and the slowest decode step (graphs are cached across sessions)
             "prefill_ms": round(statistics.mean(prefill_ms), 3) if prefill_ms else None,
             "max_decode_step_ms": round(statistics.mean(max_step), 3) if max_step else None,
             "config": {"model": args.model, "global_batch": B, "seq_len": args.prompt + args.gen,
                        "prompt_len": args.prompt, "gen_tokens": args.gen, "microbatches": M,
-                       "parallelism": f"pp{P}" + (f"xdp{R}" if R > 1 else ""),
+                       "parallelism": f"pp{P}" + (f"xdp{R}" if R > 1 else "")
+                       + ("-loopback-1gpu" if args.loopback_stages else ""),
                        "sampler": "greedy" if args.greedy else "T0.6/top-k40",
                        "hipgraphs": not args.no_graphs},
         }
         print(json.dumps(out), flush=True)
     if N > 1:
-        eng._close_dist()  # barrier, then tear the process groups down in order
+        if rank == 0:
+            eng.shutdown()  # stop the followers, barrier, tear the groups down in order
+        else:
+            eng.worker_loop()
     return 0
 
 

@@ -93,6 +93,28 @@ class BatchQueue {
     return groups;
   }
 
+  // Continuous batching (runtime/scheduler.py): the scheduler admits queued
+  // requests at every decode step without waiting -- up to k ids, FIFO.
+  std::vector<int64_t> try_pop(int k) {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<int64_t> out;
+    while (!q_.empty() && (int)out.size() < k) {
+      out.push_back(q_.front().id);
+      q_.pop_front();
+    }
+    popped_ += (int64_t)out.size();
+    return out;
+  }
+
+  // Idle scheduler: block until a request is queued, close(), or timeout.
+  bool wait_nonempty(double timeout_s) {
+    std::unique_lock<std::mutex> lk(mu_);
+    return cv_.wait_until(lk, std::chrono::system_clock::now() +
+                                  std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                      std::chrono::duration<double>(timeout_s > 0 ? timeout_s : 0.0)),
+                          [&] { return closed_ || !q_.empty(); });
+  }
+
   void close() {
     {
       std::lock_guard<std::mutex> g(mu_);

@@ -175,6 +175,9 @@ PYBIND11_MODULE(_runtime, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("next_groups", &BatchQueue::next_groups, py::arg("window_s"),
            py::call_guard<py::gil_scoped_release>())
+      .def("try_pop", &BatchQueue::try_pop, py::arg("k"))
+      .def("wait_nonempty", &BatchQueue::wait_nonempty, py::arg("timeout_s"),
+           py::call_guard<py::gil_scoped_release>())
       .def("close", &BatchQueue::close, py::call_guard<py::gil_scoped_release>())
       .def("drain", &BatchQueue::drain)
       .def_property_readonly("depth", &BatchQueue::depth)

@@ -233,7 +233,9 @@ class EngineConfig:
     shard_a_service: str = "llm-shard-a"
     shard_b_service: str = "llm-shard-b"
     shard_port: int = 5000
-    transport: str = "auto"  # auto | nccl | gloo | local | http
+    # auto | nccl | gloo | local | http | loopback (P stage threads on one GPU,
+    # device-async event hand-off: single-GPU rehearsal of the RCCL schedule)
+    transport: str = "auto"
     # Serving (runtime/scheduler.py): concurrent /generate requests arriving
     # within batch_window_ms share one pipeline round; a round running longer
     # than round_timeout_s marks the engine unhealthy; an HTTP request waits at
@@ -246,6 +248,14 @@ class EngineConfig:
     prefill_chunk: int = 0
     round_timeout_s: float = 600.0
     request_timeout_s: float = 900.0
+    # Prefill tokens per microbatch group per step when requests join a
+    # running batch (0 = unlimited: every waiting prompt joins at once).
+    prefill_budget: int = 0
+    # Fraction of the HBM left after the weights that the KV cache may use.
+    kv_fraction: float = 0.85
+    # Serving: record per-stage busy / bubble timing on one pipeline session
+    # in this many (0 = never) -- it costs a control-plane gather per session.
+    metrics_every: int = 16
 
     @property
     def model(self) -> ModelConfig:
@@ -273,6 +283,9 @@ class EngineConfig:
             prefill_chunk=int(_env("PREFILL_CHUNK", "0")),
             round_timeout_s=float(_env("ROUND_TIMEOUT_S", "600")),
             request_timeout_s=float(_env("REQUEST_TIMEOUT_S", "900")),
+            prefill_budget=int(_env("PREFILL_BUDGET", "0")),
+            kv_fraction=float(_env("KV_FRACTION", "0.85")),
+            metrics_every=int(_env("METRICS_EVERY", "16")),
         )
         if cfg.split_points and cfg.num_stages == 1:
             cfg.num_stages = len(cfg.split_points) + 1

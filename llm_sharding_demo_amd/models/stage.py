@@ -115,13 +115,14 @@ class StageModel:
         return self.backend.embed(ids, meta.token_pos, self.w["embed_tokens"], None)
 
     def forward(self, meta: BatchMeta, inp: torch.Tensor, all_logits: bool = False,
-                head: bool = True) -> torch.Tensor:
+                head: bool = True, head_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """inp: token ids int32 [T] (first stage) or hidden fp32 [T, H].
 
         Returns hidden fp32 [T, H] (non-last stage, or `head=False`: a
         non-final prefill chunk only fills the KV cache) or fp32 logits
         [B, vocab_padded] for the last query of each sequence (last stage;
-        [T, vocab_padded] with all_logits)."""
+        [T, vocab_padded] with all_logits; the rows `head_rows` of the packed
+        batch when given -- e.g. only the prompts whose final chunk this is)."""
         x = self.embed(inp, meta) if self.first else inp
         r = Residual(x)
         gpt2 = self.cfg.arch == "gpt2"
@@ -136,11 +137,13 @@ class StageModel:
         x = self.backend.flush(r)
         if not (self.last and head):
             return x
-        return self.head(x, meta, all_logits)
+        return self.head(x, meta, all_logits, head_rows)
 
-    def head(self, x: torch.Tensor, meta: BatchMeta, all_logits: bool = False) -> torch.Tensor:
+    def head(self, x: torch.Tensor, meta: BatchMeta, all_logits: bool = False,
+             rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         be, c = self.backend, self.cfg
-        rows = None if (all_logits or meta.is_decode) else meta.last_idx  # last query per sequence
+        if rows is None:
+            rows = None if (all_logits or meta.is_decode) else meta.last_idx  # last query per sequence
         if c.arch == "gpt2":
             xn = be.norm_rows(x, self.w["ln_f.weight"], self.w["ln_f.bias"], c.norm_eps, False, rows)
         else:

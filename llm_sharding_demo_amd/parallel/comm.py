@@ -31,6 +31,8 @@ owes on an earlier item.
 """
 from __future__ import annotations
 
+import datetime
+import pickle
 import queue
 import threading
 import time
@@ -121,6 +123,12 @@ class _DistTransport(Transport):
             if P > 1:
                 self.groups[f"r{rep}ret"] = dist.new_group([base + P - 1, base], backend=self._backend())
         self.ctrl = dist.new_group(list(range(P * R)), backend="gloo")
+        # step plans (rank 0 -> every rank) and DP token readouts (replica
+        # stage 0 -> rank 0) travel on their own gloo groups with no practical
+        # timeout: an idle server waits on them indefinitely
+        idle = datetime.timedelta(days=30)
+        self.plan_pg = dist.new_group(list(range(P * R)), backend="gloo", timeout=idle)
+        self.tok_pg = dist.new_group(list(range(P * R)), backend="gloo", timeout=idle)
 
     def _backend(self) -> str:
         raise NotImplementedError
@@ -226,6 +234,59 @@ class GlooTransport(_DistTransport):
 
 
 # ---------------------------------------------------------------------------
+# Plan channels: stage 0's scheduler -> the other stages (runtime/plan.py)
+# ---------------------------------------------------------------------------
+
+class LocalPlanChannel:
+    """In-process: one FIFO per follower stage thread."""
+
+    def __init__(self, stages: List[int]):
+        self.q = {r: queue.Queue() for r in stages}
+
+    def send(self, dst: int, obj) -> None:
+        self.q[dst].put(obj)
+
+    def recv(self, me: int, timeout: Optional[float] = None):
+        return self.q[me].get(timeout=timeout)
+
+
+class GlooPlanChannel:
+    """torch.distributed gloo p2p on a dedicated group: an object is pickled
+    (our own plan / token records, produced by this job's ranks) and sent as
+    a size message + a byte payload.  Sends are non-blocking (isend), so the
+    scheduler never waits on a slow follower; each receiver posts blocking
+    receives from its single source in FIFO order."""
+
+    def __init__(self, group, tag: int = 1):
+        import torch.distributed as dist
+
+        self.dist, self.pg, self.tag = dist, group, tag
+        self._works: List[tuple] = []
+
+    def send(self, dst: int, obj) -> None:
+        data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        n = torch.tensor([len(data)], dtype=torch.int64)
+        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        w1 = self.dist.isend(n, dst, group=self.pg, tag=self.tag)
+        w2 = self.dist.isend(buf, dst, group=self.pg, tag=self.tag + 1)
+        self._works.append((w1, w2, n, buf))
+        self._works = [w for w in self._works if not (w[0].is_completed() and w[1].is_completed())]
+
+    def recv(self, src: int):
+        n = torch.empty(1, dtype=torch.int64)
+        self.dist.recv(n, src, group=self.pg, tag=self.tag)
+        buf = torch.empty(int(n[0]), dtype=torch.uint8)
+        self.dist.recv(buf, src, group=self.pg, tag=self.tag + 1)
+        return pickle.loads(buf.numpy().tobytes())
+
+    def flush(self) -> None:
+        for w1, w2, _, _ in self._works:
+            w1.wait()
+            w2.wait()
+        self._works.clear()
+
+
+# ---------------------------------------------------------------------------
 # In-process fake transport (tests, single-process multi-stage)
 # ---------------------------------------------------------------------------
 
@@ -242,6 +303,23 @@ class LocalFabric:
         self._bcast: Dict[int, queue.Queue] = {r: queue.Queue() for r in range(num_stages)}
         self._seq: Dict[tuple, int] = {}
         self._barrier = threading.Barrier(num_stages)
+        self.failed: Optional[BaseException] = None  # a stage thread died: stop waiting on it
+
+    def get(self, key, what: str):
+        """Blocking receive from mailbox `key`, bounded by `timeout` and
+        abandoned as soon as any stage thread has failed."""
+        deadline = time.monotonic() + self.timeout
+        q = self.q(key)
+        while True:
+            if self.failed is not None:
+                raise TransportError(f"{what}: a pipeline stage failed: {self.failed}")
+            left = deadline - time.monotonic()
+            if left <= 0:
+                raise TransportError(f"{what}: timed out after {self.timeout}s")
+            try:
+                return q.get(timeout=min(0.1, left))
+            except queue.Empty:
+                continue
 
     def q(self, key) -> queue.Queue:
         with self._lock:
@@ -255,8 +333,51 @@ class LocalFabric:
             self._seq[key] = n + 1
             return n
 
-    def transport(self, rank: int) -> "LocalTransport":
-        return LocalTransport(self, rank)
+    def transport(self, rank: int, kind: str = "local") -> Transport:
+        return LoopbackTransport(self, rank) if kind == "loopback" else LocalTransport(self, rank)
+
+
+class LoopbackTransport(Transport):
+    """Device-async in-process transport: P stage threads on ONE MI355X.
+
+    `send` snapshots the tensor on the sender's stream (an async D2D copy into
+    a fresh buffer) and publishes it with a hipEvent; `irecv(...).wait()` makes
+    the receiver's stream wait on that event and copies into the receive
+    buffer -- no host synchronisation of the device anywhere, unlike
+    LocalTransport (whose send synchronises the stream).  This rehearses the
+    real RCCL schedule's ordering (stream waits, not host waits) on a single
+    GPU: the host threads only hand each other event handles."""
+
+    def __init__(self, fabric: LocalFabric, rank: int):
+        self.fabric, self.rank, self.world = fabric, rank, fabric.P
+
+    def send(self, t, dst, edge):
+        key = (edge, self.rank, dst)
+        cur = torch.cuda.current_stream(t.device)
+        buf = t.detach().clone()  # enqueued on the sender's stream
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self.fabric.q(key).put((buf, ev))
+        return SendHandle()
+
+    def irecv(self, out, src, edge):
+        key = (edge, src, self.rank)
+        fabric = self.fabric
+
+        def post():
+            buf, ev = fabric.get(key, f"stage {self.rank} waiting on {edge} from stage {src}")
+            cur = torch.cuda.current_stream(out.device)
+            cur.wait_event(ev)
+            buf.record_stream(cur)  # the sender's pool must not recycle it early
+            out.copy_(buf, non_blocking=True)
+
+        return Handle(out, None, post=post)
+
+    def broadcast_object(self, obj, src: int = 0):
+        return LocalTransport.broadcast_object(self, obj, src)
+
+    def barrier(self) -> None:
+        self.fabric._barrier.wait(timeout=self.fabric.timeout)
 
 
 class LocalTransport(Transport):
@@ -284,11 +405,7 @@ class LocalTransport(Transport):
         fabric = self.fabric
 
         def post():
-            try:
-                t = fabric.q(key).get(timeout=fabric.timeout)
-            except queue.Empty:
-                raise TransportError(f"stage {self.rank}: timed out after {fabric.timeout}s "
-                                     f"waiting on {edge} from stage {src}") from None
+            t = fabric.get(key, f"stage {self.rank} waiting on {edge} from stage {src}")
             out.copy_(t)
 
         return Handle(out, None, post=post)

@@ -1,4 +1,4 @@
-"""Pipeline-parallel decode scheduler (one worker per stage / per MI355X).
+"""Pipeline-parallel stage worker (one per stage / per MI355X).
 
 Replaces the reference's coordinator loop (`server.py:169-206`), which for
 every output token runs shard A, relays its hidden state through the
@@ -6,33 +6,27 @@ coordinator to shard B, ships all-position logits back and samples on the
 host -- strictly sequentially, so one shard is always idle and each token
 costs two HTTP round trips.
 
-Here a generation *round* is a set of sequences split into M microbatches.
-Every stage runs the same static schedule over items (step s, microbatch m):
+Here every stage executes the same sequence of `StepPlan`s (runtime/plan.py,
+decided by stage 0's scheduler).  A step has one *item* per busy microbatch
+group g; the item of group g on stage r does, in order:
 
-    steps 0..C-1       prefill chunks (C = 1 unless the round asks for
-                       chunked prefill: each chunk carries up to `chunk`
-                       prompt tokens per sequence, aligned to the END of the
-                       prompt so the last chunk holds every sequence's last
-                       position)
-    steps C..C+G-2     decode, one token per sequence per step
+    stage 0     receive the token-return vector of g's previous item (from
+                stage P-1), rebuild the decode input rows if the group's
+                composition changed (rows joined / left)
+    all         prefill the joining sequences' prompt chunks (eager)
+                decode the group's rows: one hipGraph replay per
+                (group, bucket rows, context bucket) -- captured once, cached
+                on the worker, replayed across steps and requests
+    stage<P-1   send the boundary hidden states to stage r+1 (prefill, decode)
+    stage P-1   sample (decode rows + final prefill chunks) and send the token
+                ids back to stage 0
 
-    for s in steps:
-        for m in 0..M-1:
-            input  <- prompt chunk s (stage 0, prefill)
-                    | sampled ids of (s-1, m) from stage P-1 (stage 0, decode)
-                    | boundary hidden of (s, m) from stage r-1
-            output <- this stage's units (+ ln_f, lm_head, sampler on P-1 for
-                      the last chunk and every decode step)
-            send output -> stage r+1   (or token ids -> stage 0 from P-1)
-
-With M >= P microbatches every stage is busy in steady state (stage r works
-on microbatch (t - r) mod M at tick t).  Receives for the next item are
-posted before the current item's compute is enqueued when they target a
-different buffer, so the transfer overlaps compute; `Handle.wait()` only
-orders the compute stream behind the comm stream.  Microbatch m runs on
-HIP stream lanes[m % L], so independent microbatches overlap on the GPU.
-Decode steps after the first replay one hipGraph per microbatch: positions
-and sampler counters advance on the device inside the graph.
+With M >= P groups every stage is busy in steady state (stage r works on
+group (t - r) mod M at tick t).  Receives of the next item are posted before
+the current item's compute when they target different buffers, so the
+transfer overlaps compute; `Handle.wait()` only orders the compute stream
+behind the comm stream.  Group g runs on HIP stream lanes[g % L], so
+independent groups overlap on the GPU.
 """
 from __future__ import annotations
 
@@ -40,59 +34,23 @@ import contextlib
 import os
 import threading
 import time
-from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
 import torch
 
 from ..models.stage import StageModel
 from ..runtime.batch import BatchMeta, SamplingState
+from ..runtime.plan import GroupPlan, StepPlan
 from ..utils.tracing import trace_range
 from .comm import Handle, SendHandle, Transport
-
 
 _CAPTURE_LOCK = threading.Lock()
 
 
-@dataclass
-class MicroBatchSpec:
-    slots: List[int]
-    prompts: List[List[int]]
-    temperature: List[float]
-    top_k: List[int]
-    greedy: List[bool]
-    seeds: List[int]
-
-    @property
-    def size(self) -> int:
-        return len(self.slots)
-
-
-@dataclass
-class RoundSpec:
-    microbatches: List[MicroBatchSpec]
-    steps: int  # tokens generated per sequence (>= 1)
-    use_graphs: bool = True
-    record_timing: bool = False
-    prefill_chunk: int = 0  # prompt tokens per sequence per prefill step; 0 = whole prompt
-
-
-@dataclass
-class RoundResult:
-    tokens: List[torch.Tensor]  # per microbatch: int32 [steps, Bm] (host)
-    step_times_ms: List[float] = field(default_factory=list)
-    prefill_ms: float = 0.0
-    # per stage (record_timing rounds): {"stage", "wall_ms", "busy_ms",
-    # "busy_fraction", "items"} -- busy = union of this stage's compute
-    # intervals over both lanes; 1 - busy_fraction is the stage's bubble
-    stages: List[dict] = field(default_factory=list)
-
-
 def prefill_chunks(lens: List[int], chunk: int) -> List[Tuple[List[int], List[int]]]:
-    """(starts, qlens) per prefill chunk for prompts of `lens` tokens.  Chunks
-    are aligned to the end of each prompt: the last chunk holds every
-    sequence's final position (its logits are sampled); earlier chunks of a
-    shorter prompt may be empty."""
+    """(starts, qlens) per prefill chunk for prompts of `lens` tokens, aligned
+    to the END of each prompt: the last chunk holds every sequence's final
+    position; earlier chunks of a shorter prompt may be empty."""
     top = max(lens)
     if chunk <= 0 or chunk >= top:
         return [([0] * len(lens), list(lens))]
@@ -106,194 +64,118 @@ def prefill_chunks(lens: List[int], chunk: int) -> List[Tuple[List[int], List[in
     return out
 
 
-class _Round:
-    """Buffers, metadata and comm state of one round on one stage."""
+class SamplingView:
+    """Sampler parameters of a decode bucket: views of the group's persistent
+    per-row tensors (graph-capturable); pad rows never advance."""
 
-    def __init__(self, w: "StageWorker", spec: RoundSpec):
-        st, dev = w.stage, w.device
-        self.w, self.spec = w, spec
-        self.M, self.G = len(spec.microbatches), spec.steps
-        if self.G < 1 or self.M < 1:
-            raise ValueError("round needs >= 1 step and >= 1 microbatch")
+    def __init__(self, temperature, top_k, greedy, seeds, step, active):
+        self.temperature, self.top_k, self.greedy = temperature, top_k, greedy
+        self.seeds, self.step, self.active = seeds, step, active
+        self.num_rows = temperature.shape[0]
+
+    def uniforms(self) -> torch.Tensor:
+        from ..runtime.batch import counter_uniform
+
+        return counter_uniform(self.seeds, self.step)
+
+    def advance(self) -> None:
+        self.step.add_(self.active.to(self.step.dtype))
+
+
+class GroupState:
+    """Persistent per-(stage, group) device state: decode row metadata,
+    sampler state, input / output buffers and the group's captured graphs."""
+
+    def __init__(self, w: "StageWorker", g: int, cap: int):
+        dev, H = w.device, w.H
         i32 = dict(dtype=torch.int32, device=dev)
-        self.chunk_meta: List[List[BatchMeta]] = []   # [m][c]
-        self.chunk_ids: List[List[torch.Tensor]] = []  # stage 0: [m][c] prompt ids
-        self.dec_meta, self.samp = [], []
-        self.in_pre, self.in_dec, self.tok_in, self.tok_out = [], [], [], []
-        per_mb = []
-        for mb in spec.microbatches:
-            lens = [len(p) for p in mb.prompts]
-            if min(lens) < 1:
-                raise ValueError("empty prompt")
-            if max(lens) + self.G > st.max_seq:
-                raise ValueError(f"prompt+generation {max(lens) + self.G} exceeds max_seq {st.max_seq}")
-            per_mb.append((lens, prefill_chunks(lens, spec.prefill_chunk)))
-        # every microbatch runs the same number of steps: shorter prompts get
-        # leading empty chunks
-        C = max(len(ch) for _, ch in per_mb)
-        for mb, (lens, chunks) in zip(spec.microbatches, per_mb):
-            empty = ([0] * mb.size, [0] * mb.size)
-            chunks = [empty] * (C - len(chunks)) + chunks
-            self.chunk_meta.append([BatchMeta.build(mb.slots, s0, q, dev) for s0, q in chunks])
-            self.dec_meta.append(BatchMeta.decode(mb.slots, lens, dev, max_ctx=max(lens) + self.G))
-            if w.last:
-                self.samp.append(SamplingState(mb.temperature, mb.top_k, mb.greedy, mb.seeds, dev))
-            if w.first:
-                self.chunk_ids.append([torch.tensor([t for p, a, n in zip(mb.prompts, s0, q)
-                                                     for t in p[a:a + n]], **i32)
-                                       for s0, q in chunks])
-                self.tok_in.append(torch.zeros(mb.size, **i32))
-                self.tok_out.append(torch.zeros(self.G, mb.size, **i32))
-            else:
-                rows = max(sum(q) for _, q in chunks)
-                self.in_pre.append(torch.empty(max(rows, 1), w.H, dtype=torch.float32, device=dev))
-                self.in_dec.append(torch.empty(mb.size, w.H, dtype=torch.float32, device=dev))
-        self.C = C
-        self.items = [(s, m) for s in range(C + self.G - 1) for m in range(self.M)]
-        self.recv: Dict[tuple, Handle] = {}
-        self.send_pending: Dict[int, SendHandle] = {}
-        self.graphs: Dict[int, tuple] = {}
-        self.step_events: List[torch.cuda.Event] = []
-        self.compute_marks: List[tuple] = []  # (start, end) events / host times per item
-
-    def rows(self, s: int, m: int) -> int:
-        return self.chunk_meta[m][s].num_tokens if s < self.C else self.spec.microbatches[m].size
-
-    def recv_target(self, s: int, m: int) -> Optional[Tuple[str, int, torch.Tensor]]:
-        """(edge, src stage, buffer) the input of item (s, m) arrives in, or None
-        when it is local (stage 0 prefill / single-stage decode) or absent."""
-        w = self.w
+        self.g, self.cap = g, cap
+        self.slots = torch.full((cap,), w.scratch_slot, **i32)
+        self.pos = torch.zeros(cap, **i32)
+        self.active = torch.zeros(cap, **i32)
+        self.cu = torch.arange(cap + 1, **i32)
+        if w.last:
+            self.temp = torch.ones(cap, dtype=torch.float32, device=dev)
+            self.topk = torch.ones(cap, **i32)
+            self.greedy = torch.ones(cap, **i32)
+            self.seeds = torch.zeros(cap, dtype=torch.int64, device=dev)
+            self.sstep = torch.zeros(cap, dtype=torch.int64, device=dev)
+            self.tokret = torch.zeros(cap, **i32)  # [decode rows | final prefill chunks]
         if w.first:
-            if s < self.C or w.P == 1:
-                return None
-            return ("ret", w.P - 1, self.tok_in[m])
-        if s < self.C:
-            n = self.rows(s, m)
-            return ("fwd", w.r - 1, self.in_pre[m][:n]) if n > 0 else None
-        return ("fwd", w.r - 1, self.in_dec[m])
-
-    def post(self, i: int) -> None:
-        if i >= len(self.items):
-            return
-        s, m = self.items[i]
-        tgt = self.recv_target(s, m)
-        if tgt is not None and (s, m) not in self.recv:
-            # posted from m's lane: the comm stream then also waits for the
-            # previous reader of this buffer (microbatch m's last compute)
-            with self.w.on_lane(m):
-                self.recv[(s, m)] = self.w.t.irecv(tgt[2], tgt[1], tgt[0])
-
-
-def _same_buffer(a: Optional[tuple], b: Optional[tuple]) -> bool:
-    return (a is not None and b is not None
-            and a[2].untyped_storage().data_ptr() == b[2].untyped_storage().data_ptr())
-
-
-class StageWorker:
-    def __init__(self, stage: StageModel, transport: Optional[Transport], stage_idx: int,
-                 num_stages: int):
-        self.stage = stage
-        self.t = transport
-        self.r = stage_idx
-        self.P = num_stages
-        self.device = stage.device
-        self.first = stage_idx == 0
-        self.last = stage_idx == num_stages - 1
-        self.H = stage.cfg.hidden
-        # Each stage worker owns a non-blocking stream: no device-wide syncs, so
-        # one stage may capture a hipGraph while another (same GPU) keeps running.
-        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
-        # Microbatch "lanes": microbatch m of this stage runs on lanes[m % L], so
-        # independent microbatches overlap on the GPU -- one's latency-bound
-        # phases (small GEMMs, split-K tails) run beside another's bandwidth-
-        # bound ones (attention over the KV cache).  Each lane has its own
-        # split-K ticket counters in the backend.
-        self.last_stats: Optional[dict] = None  # per-stage timing of the last timed round
-        n_lanes = int(os.environ.get("LSD_LANES", "2"))
-        self.lanes = ([torch.cuda.Stream(self.device) for _ in range(n_lanes)]
-                      if self.device.type == "cuda" else [])
-
-    def on_lane(self, m: int):
-        if not self.lanes:
-            return contextlib.nullcontext()
-        return torch.cuda.stream(self.lanes[m % len(self.lanes)])
-
-    # ------------------------------------------------------------------
-    def _sync(self) -> None:
-        if self.stream is not None:
-            self.stream.synchronize()
-
-    def run_round(self, spec: RoundSpec) -> Optional[RoundResult]:
-        if self.stream is None:
-            return self._run_round(spec)
-        self.stream.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self.stream):
-            res = self._run_round(spec)
-        torch.cuda.current_stream(self.device).wait_stream(self.stream)
-        return res
-
-    def _run_round(self, spec: RoundSpec) -> Optional[RoundResult]:
-        dev, P = self.device, self.P
-        R = _Round(self, spec)
-        L = max(1, len(self.lanes))
-        for lane in self.lanes:
-            lane.wait_stream(torch.cuda.current_stream(dev))
-        # kernels size their grids for the lanes that actually run side by side
-        self.stage.backend.concurrency = min(L, R.M)
-
-        t_start = time.perf_counter()
-        timing = spec.record_timing
-        t0_ev = None
-        if timing and dev.type == "cuda":
-            t0_ev = torch.cuda.Event(enable_timing=True)
-            t0_ev.record()
-        R.post(0)
-        for i, (s, m) in enumerate(R.items):
-            with self.on_lane(m), trace_range(f"stage{self.r}/step{s}/mb{m}"):
-                self._item(R, i, s, m)
-        # Stage 0 still owes the receive of the final step's tokens.
-        if self.first and P > 1:
-            for m in range(R.M):
-                with self.on_lane(m):
-                    self.t.irecv(R.tok_in[m], P - 1, "ret").wait()
-                    R.tok_out[m][R.G - 1].copy_(R.tok_in[m])
-        for h in R.send_pending.values():
-            h.wait()
-        for lane in self.lanes:
-            torch.cuda.current_stream(dev).wait_stream(lane)
-        if spec.record_timing and self.first and dev.type == "cuda":
-            ev = torch.cuda.Event(enable_timing=True)
-            with self.on_lane(0):
-                ev.record()
-            R.step_events.append(ev)
-        t1_ev = None
-        if t0_ev is not None:
-            t1_ev = torch.cuda.Event(enable_timing=True)
-            t1_ev.record()
-        self._sync()
-        elapsed = (time.perf_counter() - t_start) * 1e3
-        self.last_stats = self._stage_stats(R, t0_ev, t1_ev, t_start, elapsed) if timing else None
-        if not self.first:
-            return None
-        res = RoundResult(tokens=[t.cpu() for t in R.tok_out])
-        ev = R.step_events
-        if ev:
-            ts = [ev[k].elapsed_time(ev[k + 1]) for k in range(len(ev) - 1)]
-            res.prefill_ms = sum(ts[:R.C])
-            res.step_times_ms = ts[R.C:]
+            # decode input ids; with P > 1 also the token-return receive buffer
+            self.tin = self.tokret if w.P == 1 else torch.zeros(cap, **i32)
         else:
-            res.prefill_ms = elapsed
-        if self.last_stats is not None:
-            res.stages = [self.last_stats]
-        return res
+            self.hd = torch.empty(cap, H, dtype=torch.float32, device=dev)  # decode hidden in/out
+        self.hp: Optional[torch.Tensor] = None  # prefill hidden receive buffer (grown)
+        self.graphs: Dict[tuple, tuple] = {}
+        self.seen: set = set()
+        self._metas: Dict[tuple, BatchMeta] = {}
+        self.rows_n = 0
 
-    def _stage_stats(self, R: _Round, t0_ev, t1_ev, t_start: float, elapsed: float) -> dict:
-        if t0_ev is not None:
-            iv = sorted((t0_ev.elapsed_time(a), t0_ev.elapsed_time(b)) for a, b in R.compute_marks)
-            wall = t0_ev.elapsed_time(t1_ev)
-        else:  # CPU: compute is synchronous, host clocks are the compute intervals
-            iv = sorted(((a - t_start) * 1e3, (b - t_start) * 1e3) for a, b in R.compute_marks)
-            wall = elapsed
+    def ensure_tokret(self, w: "StageWorker", n: int) -> None:
+        """Grow the token-return vector to >= n entries (prefill finals ride
+        behind the decode rows).  Growing drops the captured graphs that
+        write into it (rare: only when a step finishes more prompts than any
+        step before)."""
+        buf = self.tokret if w.last else self.tin
+        if buf.numel() >= n:
+            return
+        new = torch.zeros(max(n, 2 * buf.numel()), dtype=torch.int32, device=buf.device)
+        new[: buf.numel()].copy_(buf)
+        if w.last:
+            self.tokret = new
+        if w.first:
+            self.tin = new
+        self.graphs.clear()
+        self.seen.clear()
+
+    def meta(self, b: int, ctxb: int) -> BatchMeta:
+        key = (b, ctxb)
+        m = self._metas.get(key)
+        if m is None:
+            m = BatchMeta(token_slots=self.slots[:b], token_pos=self.pos[:b],
+                          seq_slots=self.slots[:b], q_start=self.pos[:b], cu_q=self.cu[: b + 1],
+                          last_idx=self.cu[:b], num_tokens=b, num_seqs=b, max_q=1,
+                          max_ctx=ctxb, is_decode=True, host_qlens=[1] * b,
+                          active=self.active[:b])
+            self._metas[key] = m
+        return m
+
+    def samp(self, b: int) -> SamplingView:
+        return SamplingView(self.temp[:b], self.topk[:b], self.greedy[:b], self.seeds[:b],
+                            self.sstep[:b], self.active[:b])
+
+
+class StepStats:
+    """Per-stage busy / bubble accounting over timed steps (hipEvents on the
+    GPU, host clocks on CPU)."""
+
+    def __init__(self, dev: torch.device):
+        self.dev = dev
+        self.marks: List[tuple] = []
+        self.t0_ev = None
+        self.t_start = time.perf_counter()
+        if dev.type == "cuda":
+            self.t0_ev = torch.cuda.Event(enable_timing=True)
+            self.t0_ev.record()
+
+    def mark(self):
+        if self.dev.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.perf_counter()
+
+    def summary(self, stage: int) -> dict:
+        if self.dev.type == "cuda":
+            t1 = torch.cuda.Event(enable_timing=True)
+            t1.record()
+            t1.synchronize()
+            iv = sorted((self.t0_ev.elapsed_time(a), self.t0_ev.elapsed_time(b)) for a, b in self.marks)
+            wall = self.t0_ev.elapsed_time(t1)
+        else:
+            iv = sorted(((a - self.t_start) * 1e3, (b - self.t_start) * 1e3) for a, b in self.marks)
+            wall = (time.perf_counter() - self.t_start) * 1e3
         busy, cur = 0.0, None
         for a, b in iv:
             if cur is None or a > cur[1]:
@@ -304,94 +186,346 @@ class StageWorker:
                 cur[1] = max(cur[1], b)
         if cur is not None:
             busy += cur[1] - cur[0]
-        return {"stage": self.r, "wall_ms": round(wall, 3), "busy_ms": round(busy, 3),
+        return {"stage": stage, "wall_ms": round(wall, 3), "busy_ms": round(busy, 3),
                 "busy_fraction": round(busy / wall, 4) if wall > 0 else 0.0, "items": len(iv)}
 
-    def _body(self, R: _Round, s: int, m: int, inp):
-        """Compute of item (s, m); returns what goes downstream (None: nothing)."""
-        st = self.stage
-        st.backend.lane = m % max(1, len(self.lanes))
-        prefill = s < R.C
-        if prefill and R.rows(s, m) == 0:  # this microbatch's prompts end before chunk s
-            return None
-        meta = R.chunk_meta[m][s] if prefill else R.dec_meta[m]
-        sample = self.last and (not prefill or s == R.C - 1)
-        out = st.forward(meta, inp, head=sample or not self.last)
-        if not prefill:
-            R.dec_meta[m].advance()
-        if sample:
-            tok = st.backend.sample(out, R.samp[m], st.cfg.vocab_size)
-            R.samp[m].advance()
-            return tok
-        return None if self.last else out
 
-    def _item(self, R: _Round, i: int, s: int, m: int) -> None:
-        """One (step, microbatch) of the static schedule, on microbatch m's lane."""
-        P = self.P
-        if R.spec.record_timing and m == 0 and self.device.type == "cuda":
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            R.step_events.append(ev)
-        # --- input
-        if (s, m) in R.recv:
-            inp = R.recv.pop((s, m)).wait()
-        elif self.first:
-            inp = R.chunk_ids[m][s] if s < R.C else R.tok_in[m]
-        elif R.recv_target(s, m) is None:
-            inp = None  # empty prefill chunk of this microbatch
-        else:
-            raise RuntimeError(f"stage {self.r}: no input posted for {(s, m)}")
-        if self.first and s >= R.C:
-            R.tok_out[m][s - R.C].copy_(inp)
-        # Post the next receive before enqueueing this compute when it
-        # targets a different buffer (overlap); otherwise after.
-        cur = R.recv_target(s, m)
-        nxt = R.recv_target(*R.items[i + 1]) if i + 1 < len(R.items) else None
-        early = nxt is not None and not _same_buffer(cur, nxt)
-        if early:
-            R.post(i + 1)
-        # --- the previous send of this microbatch's static output must be done
-        if m in R.send_pending:
-            R.send_pending.pop(m).wait()
-        # --- compute
-        use_graph = R.spec.use_graphs and self.device.type == "cuda" and s >= R.C + 1
-        mark = self._mark() if R.spec.record_timing else None
-        if use_graph:
-            if m not in R.graphs:
-                R.graphs[m] = self._capture(lambda s=s, m=m, inp=inp: self._body(R, s, m, inp))
-            g, out = R.graphs[m]
-            g.replay()
-        else:
-            out = self._body(R, s, m, inp)
-        if mark is not None:
-            R.compute_marks.append((mark, self._mark()))
-        if not early:
-            R.post(i + 1)
-        # --- output
-        if out is None:
-            return
-        if self.last:
-            if P == 1:
-                R.tok_in[m].copy_(out)
-                if s == R.C + R.G - 2:
-                    R.tok_out[m][R.G - 1].copy_(out)
-            else:
-                R.send_pending[m] = self.t.send(out, 0, "ret")
-        else:
-            R.send_pending[m] = self.t.send(out, self.r + 1, "fwd")
+class StageWorker:
+    def __init__(self, stage: StageModel, transport: Optional[Transport], stage_idx: int,
+                 num_stages: int, scratch_slot: int = 0, compat_slot: int = 0):
+        self.stage = stage
+        self.t = transport
+        self.r = stage_idx
+        self.P = num_stages
+        self.device = stage.device
+        self.first = stage_idx == 0
+        self.last = stage_idx == num_stages - 1
+        self.H = stage.cfg.hidden
+        self.scratch_slot, self.compat_slot = scratch_slot, compat_slot
+        self.use_graphs = True
+        # Each stage worker owns a non-blocking stream: no device-wide syncs, so
+        # one stage may capture a hipGraph while another (same GPU) keeps running.
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        # Group "lanes": group g of this stage runs on lanes[g % L], so
+        # independent groups overlap on the GPU -- one's latency-bound
+        # phases (small GEMMs, split-K tails) run beside another's bandwidth-
+        # bound ones (attention over the KV cache).  Each lane has its own
+        # split-K ticket counters in the backend.
+        n_lanes = int(os.environ.get("LSD_LANES", "2"))
+        self.lanes = ([torch.cuda.Stream(self.device) for _ in range(n_lanes)]
+                      if self.device.type == "cuda" else [])
+        self.groups: Dict[int, GroupState] = {}
+        self.cap = 1
+        self.send_pending: Dict[int, List[SendHandle]] = {}
+        self.recv: Dict[tuple, List[Handle]] = {}
+        self.captures = 0          # hipGraph captures so far (cache effectiveness)
+        self.stats: Optional[StepStats] = None
+        self.last_stats: Optional[dict] = None
+        self.step_events: List[tuple] = []   # stage 0: (step, event) at each step start
+        self.readout = None        # stage 0: callable(step, plan, ret_tensor) for token readout
 
-    def _mark(self):
-        """Timestamp on the current (lane) stream: a timing event on the GPU,
-        the host clock on CPU."""
+    # ------------------------------------------------------------------
+    def configure(self, groups: int, cap: int) -> None:
+        """(Re)create the persistent group states (engine idle only)."""
+        self.sync()
+        self.cap = cap
+        self.groups = {g: GroupState(self, g, cap) for g in range(groups)}
+        self.send_pending.clear()
+        self.recv.clear()
+
+    def on_lane(self, g: int):
+        if not self.lanes:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(self.lanes[g % len(self.lanes)])
+
+    def sync(self) -> None:
         if self.device.type == "cuda":
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            return ev
-        return time.perf_counter()
+            for h in (h for hs in self.send_pending.values() for h in hs):
+                h.wait()
+            self.send_pending.clear()
+            for lane in self.lanes:
+                lane.synchronize()
+            if self.stream is not None:
+                self.stream.synchronize()
+
+    # ------------------------------------------------------------------
+    # timing
+    def start_stats(self) -> None:
+        self.stats = StepStats(self.device)
+
+    def end_stats(self) -> Optional[dict]:
+        if self.stats is None:
+            return None
+        self.last_stats = self.stats.summary(self.r)
+        self.stats = None
+        return self.last_stats
+
+    # ------------------------------------------------------------------
+    def run_step(self, plan: StepPlan, nxt: Optional[StepPlan] = None) -> None:
+        """Execute this stage's part of one step.  `nxt` (the following step's
+        plan, when already known) lets the last item post the next step's
+        first receive ahead of its compute."""
+        if self.stream is None:
+            return self._run_step(plan, nxt)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            self._run_step(plan, nxt)
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+    def _items(self, plan: Optional[StepPlan]) -> List[GroupPlan]:
+        if plan is None or plan.end or plan.stop:
+            return []
+        return [gp for gp in plan.groups if self._touches(gp)]
+
+    def _touches(self, gp: GroupPlan) -> bool:
+        if gp.kind == "fwd_b":
+            return self.r > 0
+        return gp.has_work or (self.first and gp.ret > 0)
+
+    def _run_step(self, plan: StepPlan, nxt: Optional[StepPlan]) -> None:
+        items = self._items(plan)
+        following = self._items(nxt)
+        L = max(1, len(self.lanes))
+        for lane in self.lanes:
+            lane.wait_stream(torch.cuda.current_stream(self.device))
+        self.stage.backend.concurrency = max(1, min(L, sum(1 for gp in items if gp.has_work)))
+        if self.first and plan.timing and self.device.type == "cuda":
+            with self.on_lane(0):
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+            self.step_events.append((plan.step, ev))
+        if items:
+            self._post(items[0])
+        for i, gp in enumerate(items):
+            nx = items[i + 1] if i + 1 < len(items) else (following[0] if following else None)
+            with self.on_lane(gp.g), trace_range(f"stage{self.r}/step{plan.step}/g{gp.g}"):
+                self._item(plan, gp, nx)
+        for lane in self.lanes:
+            torch.cuda.current_stream(self.device).wait_stream(lane)
+
+    # ------------------------------------------------------------------
+    # receives
+    def _recv_targets(self, gp: GroupPlan) -> List[Tuple[str, int, torch.Tensor]]:
+        """(edge, src stage, buffer) of every receive of item gp, in order."""
+        gs = self.groups[gp.g]
+        if gp.kind == "fwd_b":
+            if self.r == 0:
+                return []
+            return [("fwd", self.r - 1, self._hp(gs, gp.fwd_rows))]
+        if self.first:
+            if self.P > 1 and gp.ret > 0:
+                gs.ensure_tokret(self, gp.ret)
+                return [("ret", self.P - 1, gs.tin[: gp.ret])]
+            return []
+        out = []
+        T = gp.prefill_tokens
+        if T > 0:
+            out.append(("fwd", self.r - 1, self._hp(gs, T)))
+        if gp.b > 0:
+            out.append(("fwd", self.r - 1, gs.hd[: gp.b]))
+        return out
+
+    def _hp(self, gs: GroupState, T: int) -> torch.Tensor:
+        if gs.hp is None or gs.hp.shape[0] < T:
+            n = max(T, 2 * gs.hp.shape[0]) if gs.hp is not None else T
+            gs.hp = torch.empty(n, self.H, dtype=torch.float32, device=self.device)
+        return gs.hp[:T]
+
+    def _post(self, gp: Optional[GroupPlan]) -> None:
+        if gp is None or gp.g in {k[0] for k in self.recv}:
+            return
+        tg = self._recv_targets(gp)
+        if not tg:
+            return
+        with self.on_lane(gp.g):
+            # a send of this group's previous item may still read the buffer
+            # we are about to receive into (middle stages send their receive
+            # buffer: the residual stream is updated in place) -- order the
+            # receive behind it (stream-level wait, no host sync)
+            for h in self.send_pending.pop(gp.g, []):
+                h.wait()
+            self.recv[(gp.g, id(gp))] = [self.t.irecv(buf, src, edge) for edge, src, buf in tg]
+
+    def _take_recv(self, gp: GroupPlan) -> List[torch.Tensor]:
+        hs = self.recv.pop((gp.g, id(gp)), None)
+        if hs is None:
+            if self._recv_targets(gp):
+                raise RuntimeError(f"stage {self.r}: no receive posted for group {gp.g}")
+            return []
+        return [h.wait() for h in hs]
+
+    @staticmethod
+    def _buffers(tg) -> set:
+        return {t[2].untyped_storage().data_ptr() for t in tg}
+
+    # ------------------------------------------------------------------
+    def _item(self, plan: StepPlan, gp: GroupPlan, nx: Optional[GroupPlan]) -> None:
+        st, gs = self.stage, self.groups[gp.g]
+        st.backend.lane = gp.g % max(1, len(self.lanes))
+        ins = self._take_recv(gp)
+        # post the next item's receives before this compute when they target
+        # other buffers (overlap); otherwise after
+        early = (nx is not None and nx.g != gp.g
+                 and not (self._buffers(self._recv_targets(nx)) & self._buffers(self._recv_targets(gp))))
+        if early:
+            self._post(nx)
+        # outputs of this group's previous item must have left before we overwrite them
+        for h in self.send_pending.pop(gp.g, []):
+            h.wait()
+        mark = self.stats.mark() if (self.stats is not None and plan.timing) else None
+        if gp.kind == "fwd_b":
+            self._fwd_b(gp, ins)
+        else:
+            self._step_item(plan, gp, gs, ins)
+        if mark is not None:
+            self.stats.marks.append((mark, self.stats.mark()))
+        if not early:
+            self._post(nx)
+
+    def _step_item(self, plan: StepPlan, gp: GroupPlan, gs: GroupState, ins) -> None:
+        st, be = self.stage, self.stage.backend
+        k = 0
+        # --- stage 0: the previous item's token-return vector
+        if self.first:
+            ret = None
+            if gp.ret > 0:
+                ret = ins[0] if self.P > 1 else gs.tin[: gp.ret]
+                k = 1
+                if self.readout is not None:
+                    self.readout(plan, gp, ret)
+        # --- composition change: rewrite the decode rows' state
+        if gp.rows is not None:
+            self._apply_rows(gp, gs)
+        sends: List[torch.Tensor] = []
+        finals = None
+        # --- prefill chunks of joining sequences (eager)
+        if gp.chunks:
+            x = self._prefill(gp, gs, ins[k] if not self.first else None)
+            if not self.first:
+                k += 1
+            if self.last:
+                finals = x
+            elif x is not None:
+                sends.append(x)
+        # --- decode rows (hipGraph per (bucket, context bucket))
+        if gp.b > 0:
+            inp = gs.tin[: gp.b] if self.first else ins[k]
+            out = self._decode(gp, gs, inp)
+            if not self.last:
+                sends.append(out)
+        if self.last:
+            J = gp.n_final
+            nret = gp.b + J
+            if J:
+                gs.ensure_tokret(self, nret)
+                gs.tokret[gp.b: nret].copy_(finals)
+            if nret and self.P > 1:
+                self.send_pending.setdefault(gp.g, []).append(self.t.send(gs.tokret[:nret], 0, "ret"))
+        else:
+            for x in sends:
+                self.send_pending.setdefault(gp.g, []).append(self.t.send(x, self.r + 1, "fwd"))
+
+    def _apply_rows(self, gp: GroupPlan, gs: GroupState) -> None:
+        """New composition: rows [0, n) from the plan, pad rows [n, b) idle on
+        the scratch slot.  Stage 0 also gathers the rows' input token ids out
+        of the token-return vector (kept rows move, joined rows take their
+        prefill sample)."""
+        dev, rows = self.device, gp.rows
+        n, b = gp.n, max(gp.b, gp.n)
+        pad = b - n
+        sl = [r.slot for r in rows] + [self.scratch_slot] * pad
+        pos = [r.pos for r in rows] + [0] * pad
+        act = [1] * n + [0] * pad
+        if b == 0:
+            return
+        gs.rows_n = n
+        gs.slots[:b].copy_(_h2d(sl, torch.int32, dev), non_blocking=True)
+        gs.pos[:b].copy_(_h2d(pos, torch.int32, dev), non_blocking=True)
+        gs.active[:b].copy_(_h2d(act, torch.int32, dev), non_blocking=True)
+        if self.last:
+            gs.temp[:b].copy_(_h2d([r.temperature for r in rows] + [1.0] * pad, torch.float32, dev),
+                              non_blocking=True)
+            gs.topk[:b].copy_(_h2d([r.top_k for r in rows] + [1] * pad, torch.int32, dev),
+                              non_blocking=True)
+            gs.greedy[:b].copy_(_h2d([1 if r.greedy else 0 for r in rows] + [1] * pad, torch.int32,
+                                     dev), non_blocking=True)
+            gs.seeds[:b].copy_(_h2d([r.seed for r in rows] + [0] * pad, torch.int64, dev),
+                               non_blocking=True)
+            gs.sstep[:b].copy_(_h2d([r.step for r in rows] + [0] * pad, torch.int64, dev),
+                               non_blocking=True)
+        if self.first:
+            src = _h2d([r.src for r in rows] + [0] * pad, torch.int64, dev)
+            gathered = gs.tin.index_select(0, src.to(dev, non_blocking=True))
+            gs.tin[:b].copy_(gathered)
+
+    def _prefill(self, gp: GroupPlan, gs: GroupState, inp: Optional[torch.Tensor]):
+        st, be, dev = self.stage, self.stage.backend, self.device
+        ch = gp.chunks
+        meta = BatchMeta.build([c.slot for c in ch], [c.start for c in ch], [c.qlen for c in ch], dev)
+        if self.first:
+            inp = _h2d([t for c in ch for t in c.ids], torch.int32, dev).to(dev, non_blocking=True)
+        finals = [i for i, c in enumerate(ch) if c.final]
+        if not self.last:
+            return st.forward(meta, inp, head=False)
+        if not finals:
+            st.forward(meta, inp, head=False)  # KV cache only
+            return None
+        rows = meta.last_idx.index_select(0, torch.tensor(finals, dtype=torch.long, device=dev))
+        logits = st.forward(meta, inp, head=True, head_rows=rows)
+        fc = [ch[i] for i in finals]
+        samp = SamplingState([c.temperature for c in fc], [c.top_k for c in fc],
+                             [c.greedy for c in fc], [c.seed for c in fc], dev)
+        return be.sample(logits, samp, st.cfg.vocab_size)
+
+    def _decode(self, gp: GroupPlan, gs: GroupState, inp: torch.Tensor) -> torch.Tensor:
+        key = (gp.b, gp.ctxb)
+
+        def body():
+            meta = gs.meta(gp.b, gp.ctxb)
+            out = self.stage.forward(meta, inp, head=True)
+            meta.advance()
+            if not self.last:
+                return out
+            samp = gs.samp(gp.b)
+            tok = self.stage.backend.sample(out, samp, self.stage.cfg.vocab_size)
+            samp.advance()
+            gs.tokret[: gp.b].copy_(tok)
+            return gs.tokret[: gp.b]
+
+        graphs = self.use_graphs and self.device.type == "cuda"
+        if not graphs:
+            return body()
+        if key in gs.graphs:
+            g, out = gs.graphs[key]
+            g.replay()
+            return out
+        if key not in gs.seen:  # first use: eager (allocates workspaces outside capture)
+            gs.seen.add(key)
+            return body()
+        gs.graphs[key] = self._capture(body)
+        self.captures += 1
+        g, out = gs.graphs[key]
+        g.replay()
+        return out
+
+    def _fwd_b(self, gp: GroupPlan, ins) -> None:
+        """Compat /forward_b on stages 1..P-1: full-sequence forward of the
+        hidden rows received from stage 0 on the compat KV slot; the last
+        stage returns all-position fp32 logits to stage 0."""
+        st = self.stage
+        T = gp.fwd_rows
+        meta = BatchMeta.build([self.compat_slot], [0], [T], self.device)
+        x = ins[0]
+        if self.last:
+            out = st.forward(meta, x, all_logits=True)
+            self.send_pending.setdefault(gp.g, []).append(self.t.send(out, 0, "ret"))
+        else:
+            out = st.forward(meta, x)
+            self.send_pending.setdefault(gp.g, []).append(self.t.send(out, self.r + 1, "fwd"))
 
     # ------------------------------------------------------------------
     def _capture(self, fn):
-        """Capture one decode step (this stage's forward for one microbatch,
+        """Capture one decode step (this stage's forward for one group bucket,
         plus sampling on the last stage) into a hipGraph."""
         # capture_begin/end directly: torch.cuda.graph() does a device-wide
         # synchronize on entry, which is illegal while a sibling stage thread on
@@ -408,3 +542,12 @@ class StageWorker:
                     g.capture_end()
         torch.cuda.current_stream(self.device).wait_stream(s)
         return g, out
+
+
+def _h2d(vals, dtype, dev) -> torch.Tensor:
+    """Host tensor for an async copy to `dev` (pinned when `dev` is a GPU;
+    the caching host allocator keeps it alive until the copy has run)."""
+    t = torch.tensor(vals, dtype=dtype)
+    if dev.type == "cuda":
+        t = t.pin_memory()
+    return t

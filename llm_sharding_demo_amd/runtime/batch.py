@@ -34,6 +34,9 @@ class BatchMeta:
     max_ctx: int  # upper bound on q_start + qlen (host-side, for grid sizing)
     is_decode: bool
     host_qlens: Optional[List[int]] = None  # per-sequence query counts (host copy)
+    # decode buckets (runtime/plan.py): 1 for real rows, 0 for pad rows, which
+    # never advance (they stay on position 0 of the scratch KV slot)
+    active: Optional[torch.Tensor] = None
 
     @staticmethod
     def build(slots: Sequence[int], starts: Sequence[int], qlens: Sequence[int],
@@ -75,9 +78,12 @@ class BatchMeta:
                          max_ctx=max_ctx, is_decode=True, host_qlens=[1] * B)
 
     def advance(self) -> None:
-        """Decode only: every sequence moves one position forward (in place)."""
+        """Decode only: every (active) sequence moves one position forward (in place)."""
         assert self.is_decode
-        self.token_pos.add_(1)
+        if self.active is None:
+            self.token_pos.add_(1)
+        else:
+            self.token_pos.add_(self.active)
 
 
 class SamplingState:

@@ -1,47 +1,60 @@
-"""Inference engine: request batching, slot management, round execution.
+"""Inference engine: stages, KV slots, the continuous-batching driver loop.
 
 Plays the reference coordinator's role (`server.py:154-210`: tokenize ->
 decode loop -> detokenize), but the decode loop runs inside the stage
-workers (parallel/pipeline.py) and only the final token ids come back.
+workers (parallel/pipeline.py) and only sampled token ids come back.
 
 Execution modes
-  * local  -- all P stages live in this process.  P == 1 runs inline; P > 1
-              runs one thread per stage over the in-memory LocalTransport
-              (each stage may sit on its own device).  Used on CPU (tests)
-              and for single-GPU runs.
+  * local  -- all P stages live in this process.  Stage 0 runs on the
+              driving thread; stages 1..P-1 are persistent worker threads fed
+              with step plans through in-process queues, exchanging tensors
+              over the in-memory LocalTransport (each stage may sit on its own
+              device).  Used on CPU (tests) and for single-GPU runs.
   * dist   -- one process per MI355X under torchrun; rank r owns stage
               r % P of pipeline replica r // P (dp_replicas R, world = P*R).
-              Rank 0 is the coordinator and also stage 0 of replica 0; other
-              ranks sit in `worker_loop()` and receive per-replica round specs
-              over a gloo control group.  Data moves over RCCL p2p
-              (NcclTransport), one set of edge communicators per replica.
+              Rank 0 runs the scheduler (and stage 0 of replica 0); every
+              other rank sits in `worker_loop()` executing the step plans it
+              receives on the gloo plan channel.  Data moves over RCCL p2p
+              (NcclTransport), one set of edge communicators per replica;
+              replica stage-0 ranks ship their sampled ids back to rank 0.
+
+Every request goes through `Scheduler` (runtime/scheduler.py): requests join
+and leave microbatch groups at decode-step boundaries (iteration-level
+batching), so a short request finishes while a long one keeps decoding.
 """
 from __future__ import annotations
 
 import logging
 import os
+import queue
 import random
+import statistics
 import threading
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import torch
 
 from ..config import EngineConfig, SamplingParams
 from ..models.stage import StageModel
-from ..parallel.comm import LocalFabric, Transport, init_distributed, make_dist_transport
+from ..parallel.comm import (GlooPlanChannel, LocalFabric, LocalPlanChannel, Transport,
+                             TransportError, init_distributed, make_dist_transport)
 from ..parallel.partition import make_unit_plan, units_to_layers
-from ..parallel.pipeline import MicroBatchSpec, RoundResult, RoundSpec, StageWorker
-from .kv_cache import SlotAllocator
+from ..parallel.pipeline import StageWorker
+from .kv_cache import KVCache, SlotAllocator, plan_slots
+from .plan import GroupPlan, StepPlan
+from .scheduler import Request, Scheduler
 
 log = logging.getLogger("llm_sharding_demo_amd.engine")
 
 
 @dataclass
-class GenerationOutput:
-    prompt_ids: List[int]
-    output_ids: List[int]
+class SessionStats:
+    """Timing of the last timed session (bench, sampled serving steps)."""
+    step_times_ms: List[float] = field(default_factory=list)
+    prefill_ms: float = 0.0
+    stages: List[dict] = field(default_factory=list)
 
 
 def _dtype(name: str, device: torch.device) -> torch.dtype:
@@ -67,33 +80,48 @@ class Engine:
         if mode == "local" and self.R != 1:
             raise ValueError("dp_replicas > 1 needs the dist mode (one process per GPU)")
         self.replica, self.stage_idx = 0, 0
+        self.M = max(1, cfg.microbatches)                # microbatch groups per replica
+        self.group_cap = -(-cfg.max_batch // self.M)     # decode rows per group
         # stage ranges in half-layer units (parallel/partition.py); `plan` is
         # the layer view (a layer cut in half is listed in both stages)
-        mb_rows = -(-cfg.max_batch // max(1, cfg.microbatches))
         self.unit_plan = make_unit_plan(self.mcfg, self.P, cfg.split_points, cfg.split_units,
-                                        rows=mb_rows, avg_ctx=min(192, cfg.max_seq_len),
+                                        rows=self.group_cap, avg_ctx=min(192, cfg.max_seq_len),
                                         half_layers=cfg.half_layer_split)
         self.plan = units_to_layers(self.unit_plan)
         self._rng = random.Random(cfg.seed)
         self.healthy = True
         self.last_error: Optional[str] = None
-        self._lock = threading.Lock()
-        self.stats = {"requests": 0, "tokens": 0, "rounds": 0, "busy_s": 0.0}
-        self.last_round: Optional[RoundResult] = None
-        self.round_started: Optional[float] = None  # monotonic start of the running round (watchdog)
+        self._lock = threading.RLock()
+        self.round_started: Optional[float] = None  # monotonic time of the last progress (watchdog)
         self.max_seq = min(cfg.max_seq_len, self.mcfg.max_positions)
+        self.last_session: Optional[SessionStats] = None
+        self.loop_thread: Optional[threading.Thread] = None
+        self._stop_loop = threading.Event()
+        self._wake = threading.Event()  # a request was submitted (serving loop)
+        self.kv_slots = 0
 
         if mode == "local":
             if devices is None:
                 dev = resolve_device(cfg.device)
                 devices = [str(dev)] * self.P
-            self.devices = [torch.device(d) for d in devices]
+            self.devices = [_with_index(torch.device(d)) for d in devices]
+            self.kv_slots = self._kv_slots(self.devices)
             self.stages = [self._build_stage(i, self.devices[i]) for i in range(self.P)]
             self.fabric = LocalFabric(self.P, fault=fault) if self.P > 1 else None
-            self.workers = [StageWorker(st, self.fabric.transport(i) if self.fabric else None, i, self.P)
+            # "loopback": device-async event hand-off between stage threads on
+            # GPUs (single-GPU rehearsal of the RCCL schedule); else host queues
+            kind = "loopback" if (cfg.transport == "loopback" and self.devices[0].type == "cuda") else "local"
+            self.workers = [self._worker(st, self.fabric.transport(i, kind) if self.fabric else None, i)
                             for i, st in enumerate(self.stages)]
             self.rank = 0
             self.transport: Optional[Transport] = None
+            self.plan_ch = LocalPlanChannel(list(range(1, self.P)))
+            self._follow_err: Optional[BaseException] = None
+            self._stats_q: "queue.Queue" = queue.Queue()
+            self._followers = [threading.Thread(target=self._local_follower, args=(i,), daemon=True,
+                                                name=f"lsd-stage{i}") for i in range(1, self.P)]
+            for t in self._followers:
+                t.start()
         elif mode == "dist":
             import torch.distributed as dist
 
@@ -107,94 +135,387 @@ class Engine:
             self.devices = [dev]
             self.transport = make_dist_transport(self.P, kind, dev, self.R)
             self.replica, self.stage_idx = self.transport.replica, self.transport.rank
+            self.kv_slots = self._kv_slots([dev], collective=True)
             stage = self._build_stage(self.stage_idx, dev)
             self.stages = [stage]
-            self.workers = [StageWorker(stage, self.transport, self.stage_idx, self.P)]
+            self.workers = [self._worker(stage, self.transport, self.stage_idx)]
             self.fabric = None
+            self.plan_ch = GlooPlanChannel(self.transport.plan_pg, tag=1)
+            self.tok_ch = GlooPlanChannel(self.transport.tok_pg, tag=3)
+            self._tok_threads: List[threading.Thread] = []
+            if self.rank == 0:
+                for rep in range(1, self.R):
+                    t = threading.Thread(target=self._tok_receiver, args=(rep,), daemon=True)
+                    t.start()
+                    self._tok_threads.append(t)
+            elif self.stage_idx == 0:
+                self._tok_q: "queue.Queue" = queue.Queue()
+                t = threading.Thread(target=self._tok_shipper, daemon=True)
+                t.start()
+                self._tok_threads.append(t)
+                self.workers[0].readout = self._ship_readout
         else:
             raise ValueError(f"unknown mode {mode!r}")
-        # one KV-slot pool per pipeline replica (the coordinator allocates for all)
-        self.slot_pools = [_make_slot_allocator(self.stages[0].kv.slots) for _ in range(self.R)]
+        # one KV-slot pool per pipeline replica (the scheduler allocates for all)
+        self.slot_pools = [_make_slot_allocator(self.kv_slots) for _ in range(self.R)]
         self.slots = self.slot_pools[0]
+        self.scheduler = Scheduler(self, self.M, self.group_cap)
+        if self.rank == 0:
+            self.workers[0].readout = self.scheduler.on_readout
+        for w in self.workers:
+            w.use_graphs = cfg.use_graphs
+            w.configure(self.M, self.group_cap)
 
     # ------------------------------------------------------------------
+    def _kv_slots(self, devices, collective: bool = False) -> int:
+        """KV slots per stage: max_batch, capped by what fits the KV budget of
+        free HBM (288 GB per MI355X) after the weights.  In
+        dist mode every rank computes its own cap and all take the minimum."""
+        want = self.cfg.max_batch
+        fits = want
+        for i, dev in enumerate(devices):
+            if dev.type != "cuda":
+                continue
+            # the stage's KV layers (its attention halves)
+            a, b = self.unit_plan[self.stage_idx if collective else i]
+            n_kv_layers = sum(1 for u in range(a, b) if u % 2 == 0)
+            per_stage_w = self._weight_bytes(self.stage_idx if collective else i)
+            fits = min(fits, plan_slots(want + 2, n_kv_layers, self.mcfg.n_kv_heads, self.max_seq,
+                                        self.mcfg.head_dim, dev, reserve=per_stage_w,
+                                        fraction=self.cfg.kv_fraction) - 2)
+        if collective:
+            import torch.distributed as dist
+
+            t = torch.tensor([fits], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.transport.ctrl)
+            fits = int(t[0])
+        if fits < 1:
+            raise MemoryError("KV cache: not even one sequence fits the HBM budget")
+        if fits < want:
+            log.warning("KV budget: %d of %d requested slots fit", fits, want)
+        return fits
+
+    def _weight_bytes(self, i: int) -> int:
+        mc = self.mcfg
+        a, b = self.unit_plan[i]
+        per_layer = mc.block_params() * 2
+        n = per_layer * (b - a) // 2
+        if i == 0:
+            n += mc.embed_params() * 2
+        if i == self.P - 1:
+            n += mc.lm_head_params() * 2 * 2  # weight + padded copy
+        return n
+
     def _build_stage(self, i: int, device: torch.device) -> StageModel:
         a, b = self.plan[i]
+        # +2 slots: scratch (pad rows of decode buckets) and compat forwards
         return StageModel(self.mcfg, a, b, first=(i == 0), last=(i == self.P - 1), device=device,
                           dtype=_dtype(self.cfg.dtype, device), seed=self.cfg.seed,
-                          weights_path=self.cfg.weights, max_slots=self.cfg.max_batch,
+                          weights_path=self.cfg.weights, max_slots=self.kv_slots + 2,
                           max_seq=self.max_seq, units=self.unit_plan[i])
+
+    def _worker(self, st: StageModel, t, i: int) -> StageWorker:
+        return StageWorker(st, t, i, self.P, scratch_slot=self.kv_slots,
+                           compat_slot=self.kv_slots + 1)
 
     @property
     def is_coordinator(self) -> bool:
         return self.rank == 0
 
+    def kv_info(self) -> dict:
+        st = self.stages[0]
+        return {"kv_slots": self.kv_slots, "kv_bytes_stage0": st.kv.nbytes,
+                "kv_slots_free": sum(p.available for p in self.slot_pools),
+                "group_rows": self.group_cap, "groups": self.M}
+
     # ------------------------------------------------------------------
-    def _run_rounds(self, specs: List[Optional[RoundSpec]]) -> List[Optional[RoundResult]]:
-        """One round per pipeline replica (None = replica idle this round)."""
-        if self.mode != "dist":
-            return [self._run_round(specs[0])]
-        self.transport.broadcast_object(("round", specs), src=0)
-        return self._dist_round(specs)
+    # requests
+    # ------------------------------------------------------------------
+    def _validate(self, prompt: List[int], sp: SamplingParams) -> None:
+        sp.validate()
+        if len(prompt) == 0:
+            raise ValueError("prompt must contain at least one token")
+        if len(prompt) + sp.max_new_tokens > self.max_seq:
+            raise ValueError(f"prompt ({len(prompt)}) + max_new_tokens ({sp.max_new_tokens}) "
+                             f"exceeds the context limit {self.max_seq}")
 
-    def _dist_round(self, specs) -> List[Optional[RoundResult]]:
-        spec = specs[self.replica]
-        res = self.workers[0].run_round(spec) if spec is not None else None
-        if any(sp is not None and sp.record_timing for sp in specs):
-            # per-stage busy / bubble figures of every rank, to the coordinator
-            stats = self.transport.gather_object(self.workers[0].last_stats if spec else None, dst=0)
-            if stats is not None and res is not None:
-                res.stages = [dict(st, replica=g // self.P) for g, st in enumerate(stats)
-                              if st is not None]
-        if self.R == 1:
-            return [res]
-        # stage 0 of every replica holds its replica's tokens; collect on rank 0
-        got = self.transport.gather_object(res if self.stage_idx == 0 else None, dst=0)
-        return None if got is None else [got[r * self.P] for r in range(self.R)]
+    def submit(self, prompt_ids: List[int], params: SamplingParams) -> Request:
+        """Thread-safe: queue one request; the driver loop admits it at the
+        next decode-step boundary."""
+        if self.mode == "dist" and self.rank != 0:
+            raise RuntimeError("submit() on a non-coordinator rank")
+        if not self.healthy:
+            raise RuntimeError(f"engine unhealthy: {self.last_error}")
+        self._validate(prompt_ids, params)
+        req = self.scheduler.submit(prompt_ids, params)
+        self._wake.set()
+        return req
 
-    def _run_round(self, spec: RoundSpec) -> RoundResult:
-        if self.mode == "dist":
-            return self._run_rounds([spec] + [None] * (self.R - 1))[0]
-        if self.P == 1:
-            return self.workers[0].run_round(spec)
-        results: List[Optional[RoundResult]] = [None] * self.P
-        errors: List[BaseException] = []
+    def generate_ids(self, prompts: List[List[int]], params, microbatches: Optional[int] = None,
+                     record_timing: bool = False) -> List[List[int]]:
+        """Generate continuations for token-id prompts (generated ids only).
+        Runs the driver loop on this thread unless the serving loop is up."""
+        if isinstance(params, SamplingParams):
+            params = [params] * len(prompts)
+        for p, sp in zip(prompts, params):
+            self._validate(p, sp)
+        if not self.healthy:
+            raise RuntimeError(f"engine unhealthy: {self.last_error}")
+        if microbatches and microbatches != self.M and self.loop_thread is None:
+            self.set_groups(microbatches)
+        reqs = [self.scheduler.submit(p, sp) for p, sp in zip(prompts, params)]
+        if self.loop_thread is not None:
+            return [r.wait() for r in reqs]
+        with self._lock:
+            self._drive(lambda: all(r.done for r in reqs), timing=record_timing)
+        return [r.wait(0) for r in reqs]
 
-        def run(i):
-            try:
-                if self.devices[i].type == "cuda":
-                    torch.cuda.set_device(self.devices[i])
-                results[i] = self.workers[i].run_round(spec)
-            except BaseException as e:  # propagate to caller
-                errors.append(e)
+    def set_groups(self, M: int) -> None:
+        """Re-shape the microbatch groups (only between sessions)."""
+        with self._lock:
+            if self.scheduler.has_work():
+                raise RuntimeError("cannot regroup while requests are in flight")
+            if self.mode == "dist":
+                raise RuntimeError("regrouping needs every rank: set num_microbatches instead")
+            self.M = max(1, M)
+            self.group_cap = -(-self.cfg.max_batch // self.M)
+            self.scheduler = Scheduler(self, self.M, self.group_cap)
+            self.workers[0].readout = self.scheduler.on_readout
+            for w in self.workers:
+                w.configure(self.M, self.group_cap)
 
-        threads = [threading.Thread(target=run, args=(i,), daemon=True) for i in range(self.P)]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
-        if errors:
-            raise errors[0]
-        if spec.record_timing:
-            results[0].stages = [w.last_stats for w in self.workers if w.last_stats is not None]
-        return results[0]
+    # ------------------------------------------------------------------
+    # the driver loop (stage 0 of replica 0 / rank 0)
+    # ------------------------------------------------------------------
+    def _send_plans(self, plans: Optional[List[StepPlan]], end: bool = False) -> None:
+        """Plan of every replica to every rank that executes it."""
+        for rep in range(self.R):
+            p = plans[rep] if plans is not None else StepPlan(step=-1, replica=rep, end=True,
+                                                               timing=self.scheduler.timing)
+            for r in range(self.P):
+                g = rep * self.P + r
+                if g == 0:
+                    continue
+                self.plan_ch.send(g if self.mode == "dist" else r, p)
+
+    def _drive(self, until, timing: bool = False) -> None:
+        """Run pipeline steps until `until()` (and no work is left in flight
+        that `until` depends on).  One session = plans until idle; followers
+        get an `end` marker when it goes idle."""
+        sch = self.scheduler
+        sch.timing = timing
+        w0 = self.workers[0]
+        if timing:
+            for w in self.workers:
+                w.step_events.clear()
+            sch.step_log.clear()
+            self._start_stats()
+        lag = self.P + 2  # steps the host may run ahead of the GPU readouts
+        ran = False
+        try:
+            cur = sch.build_step()
+            if cur is not None:
+                ran = True
+                self._send_plans(cur)
+            while cur is not None:
+                self._check_followers()
+                if not self.healthy:
+                    raise RuntimeError(self.last_error)
+                self.round_started = time.monotonic()
+                nxt = sch.build_step()
+                self._send_plans(nxt)
+                w0.run_step(cur[0], nxt[0] if nxt is not None else None)
+                sch.poll(block_until_step=cur[0].step - lag)
+                cur = nxt
+            # everything issued: wait for the outstanding readouts
+            while sch.readouts or not until():
+                if sch.readouts:
+                    sch.poll(block_until_step=1 << 62)
+                elif not until():
+                    # remote replicas' readouts still on their way
+                    self._check_followers()
+                    if not self.healthy:
+                        raise RuntimeError(self.last_error)
+                    time.sleep(0.0005)
+                    sch.poll()
+        except BaseException as e:
+            self.healthy = False
+            self.last_error = f"{type(e).__name__}: {e}"
+            sch.fail_all(RuntimeError(f"engine unhealthy: {self.last_error}"))
+            raise
+        finally:
+            self.round_started = None
+        if timing and ran:
+            self._finish_stats()
+
+    def _check_followers(self) -> None:
+        err = getattr(self, "_follow_err", None)
+        if err is not None:
+            raise err
+
+    # -- timing ------------------------------------------------------------
+    def _start_stats(self) -> None:
+        self.workers[0].start_stats()
+
+    def _finish_stats(self) -> None:
+        w0 = self.workers[0]
+        if self.devices[0].type == "cuda":
+            torch.cuda.synchronize(self.devices[0])
+        stats = [w0.end_stats()]
+        if self.mode == "local":
+            for _ in range(self.P - 1):
+                stats.append(self._stats_q.get(timeout=self.cfg.round_timeout_s))
+        else:
+            got = self.transport.gather_object(stats[0], dst=0)
+            stats = [dict(st, replica=g // self.P) for g, st in enumerate(got) if st is not None]
+        ss = SessionStats(stages=sorted([s for s in stats if s], key=lambda s: (s.get("replica", 0),
+                                                                               s["stage"])))
+        ev = w0.step_events
+        log_ = dict(self.scheduler.step_log)
+        if ev:
+            ts = [(ev[k][0], ev[k][1].elapsed_time(ev[k + 1][1])) for k in range(len(ev) - 1)]
+            ss.prefill_ms = sum(t for s, t in ts if log_.get(s))
+            ss.step_times_ms = [t for s, t in ts if not log_.get(s)]
+        self.last_session = ss
+
+    # ------------------------------------------------------------------
+    # followers
+    # ------------------------------------------------------------------
+    def _follow(self, recv, worker: StageWorker) -> bool:
+        """Execute plans until the session ends (True) or stop (False)."""
+        cur = recv()
+        started = False
+        while True:
+            if cur.stop:
+                return False
+            if cur.end:
+                if started or cur.timing:
+                    self._follower_stats(worker, cur)
+                return True
+            if cur.timing and not started:
+                worker.start_stats()
+                started = True
+            nxt = recv()
+            worker.run_step(cur, nxt if not nxt.stop else None)
+            cur = nxt
+
+    def _follower_stats(self, worker: StageWorker, end_plan: StepPlan) -> None:
+        if not end_plan.timing:
+            worker.stats = None
+            return
+        worker.sync()
+        st = worker.end_stats()
+        if self.mode == "local":
+            self._stats_q.put(st)
+        else:
+            self.transport.gather_object(st, dst=0)
+
+    def _local_follower(self, i: int) -> None:
+        w = self.workers[i]
+        try:
+            if self.devices[i].type == "cuda":
+                torch.cuda.set_device(self.devices[i])
+            while self._follow(lambda: self.plan_ch.recv(i), w):
+                pass
+        except BaseException as e:  # surfaced on the driving thread
+            log.error("stage %d failed: %s", i, e)
+            self._follow_err = e
+            if self.fabric is not None:
+                self.fabric.failed = e  # wake stages blocked on this one
+
+    def follow_session(self) -> bool:
+        """Dist followers: execute one session's plans (False on stop)."""
+        assert self.mode == "dist" and self.rank != 0
+        return self._follow(lambda: self.plan_ch.recv(0), self.workers[0])
 
     def worker_loop(self) -> None:
-        """Non-coordinator ranks: execute commands until 'stop'."""
-        assert self.mode == "dist" and self.rank != 0
+        """Non-coordinator ranks: execute plans until 'stop'."""
+        while self.follow_session():
+            pass
+        self._close_dist()
+
+    # DP: replica stage-0 ranks ship sampled ids to rank 0 --------------------
+    def _ship_readout(self, plan: StepPlan, gp: GroupPlan, ret: torch.Tensor) -> None:
+        n = gp.ret
+        if ret.is_cuda:
+            host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+            host.copy_(ret[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = ret[:n].clone(), None
+        self._tok_q.put((plan.step, (plan.replica, plan.step, gp.g), host, ev))
+
+    def _tok_shipper(self) -> None:
         while True:
-            cmd = self.transport.broadcast_object(None, src=0)
-            if cmd[0] == "round":
-                self._dist_round(cmd[1])
-            elif cmd[0] == "stop":
-                self._close_dist()
-                break
-            else:
-                raise RuntimeError(f"unknown command {cmd[0]!r}")
+            item = self._tok_q.get()
+            if item is None:
+                self.tok_ch.send(0, None)
+                self.tok_ch.flush()
+                return
+            step, key, host, ev = item
+            if ev is not None:
+                ev.synchronize()
+            self.tok_ch.send(0, (step, key, host.tolist()))
+
+    def _tok_receiver(self, rep: int) -> None:
+        src = rep * self.P
+        while True:
+            msg = self.tok_ch.recv(src)
+            if msg is None:
+                return
+            step, key, toks = msg
+            self.scheduler.push_remote_readout(step, toks, key)
+
+    # ------------------------------------------------------------------
+    # serving loop (background thread) and shutdown
+    # ------------------------------------------------------------------
+    def start_loop(self) -> None:
+        """Serve submitted requests continuously on a background thread."""
+        if self.loop_thread is not None:
+            return
+        self._stop_loop.clear()
+        self.loop_thread = threading.Thread(target=self._serve, name="lsd-engine", daemon=True)
+        self.loop_thread.start()
+
+    def _serve(self) -> None:
+        sch = self.scheduler
+        n = 0
+        while not self._stop_loop.is_set():
+            if not sch.has_work():
+                # Python-side wait: a daemon thread parked inside native code
+                # with the GIL released would abort the interpreter at exit
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            # sample the per-stage timing on one session in `metrics_every`
+            every = max(0, self.cfg.metrics_every)
+            timing = every > 0 and n % every == 0
+            n += 1
+            try:
+                with self._lock:
+                    self._drive(lambda: not sch.has_work(), timing=timing)
+            except BaseException as e:  # requests already failed by _drive
+                log.error("pipeline failed: %s", e)
+                if not self.healthy:
+                    return
+
+    def stop_loop(self) -> None:
+        self._stop_loop.set()
+        if self.loop_thread is not None:
+            self.loop_thread.join(timeout=30)
+            self.loop_thread = None
 
     def shutdown(self) -> None:
-        if self.mode == "dist" and self.rank == 0:
-            self.transport.broadcast_object(("stop",), src=0)
+        self.stop_loop()
+        if self.mode == "local":
+            for i in range(1, self.P):
+                self.plan_ch.send(i, StepPlan(step=-1, stop=True))
+            return
+        if self.rank == 0:
+            for r in range(1, self.P * self.R):
+                self.plan_ch.send(r, StepPlan(step=-1, stop=True))
+            self.plan_ch.flush()
             self._close_dist()
 
     def _close_dist(self) -> None:
@@ -203,127 +524,76 @@ class Engine:
         RCCL connection open to it."""
         import torch.distributed as dist
 
+        if self.rank != 0 and self.stage_idx == 0 and self.R > 1:
+            self._tok_q.put(None)
+            for t in self._tok_threads:
+                t.join(timeout=30)
         self.transport.barrier()
+        if self.rank == 0:
+            for t in self._tok_threads:
+                t.join(timeout=30)
         if dist.is_initialized():
             dist.destroy_process_group()
 
     # ------------------------------------------------------------------
-    def make_round(self, prompts: List[List[int]], params: List[SamplingParams], slots: List[int],
-                   microbatches: Optional[int] = None, use_graphs: Optional[bool] = None,
-                   record_timing: bool = False) -> RoundSpec:
-        n = len(prompts)
-        M = max(1, min(microbatches or self.cfg.microbatches, n))
-        steps = max(p.max_new_tokens for p in params)
-        bounds = [round(i * n / M) for i in range(M + 1)]
-        mbs = []
-        for j in range(M):
-            a, b = bounds[j], bounds[j + 1]
-            ps = params[a:b]
-            mbs.append(MicroBatchSpec(
-                slots=slots[a:b], prompts=[list(map(int, p)) for p in prompts[a:b]],
-                temperature=[p.temperature for p in ps], top_k=[p.top_k for p in ps],
-                greedy=[p.greedy for p in ps],
-                seeds=[p.seed if p.seed is not None else self._rng.getrandbits(62) for p in ps]))
-        g = self.cfg.use_graphs if use_graphs is None else use_graphs
-        return RoundSpec(microbatches=mbs, steps=steps, use_graphs=g, record_timing=record_timing,
-                         prefill_chunk=self.cfg.prefill_chunk)
-
-    def generate_ids(self, prompts: List[List[int]], params, microbatches: Optional[int] = None,
-                     record_timing: bool = False) -> List[List[int]]:
-        """Generate continuations for a list of token-id prompts.  Returns the
-        generated ids only (not including the prompt)."""
-        if isinstance(params, SamplingParams):
-            params = [params] * len(prompts)
-        for p, sp in zip(prompts, params):
-            sp.validate()
-            if len(p) == 0:
-                raise ValueError("prompt must contain at least one token")
-            if len(p) + sp.max_new_tokens > self.max_seq:
-                raise ValueError(f"prompt ({len(p)}) + max_new_tokens ({sp.max_new_tokens}) "
-                                 f"exceeds the context limit {self.max_seq}")
-        outs: List[List[int]] = [[] for _ in prompts]
-        todo = [i for i, sp in enumerate(params) if sp.max_new_tokens > 0]
-        cap, R = self.slots.capacity, self.R
-        with self._lock:
-            if not self.healthy:
-                raise RuntimeError(f"engine unhealthy: {self.last_error}")
-            for c0 in range(0, len(todo), cap * R):
-                chunk = todo[c0:c0 + cap * R]
-                # contiguous, balanced share per pipeline replica
-                parts = [chunk[round(j * len(chunk) / R): round((j + 1) * len(chunk) / R)]
-                         for j in range(R)]
-                slots = [self.slot_pools[j].alloc(len(part)) if part else []
-                         for j, part in enumerate(parts)]
-                try:
-                    specs = [self.make_round([prompts[i] for i in part], [params[i] for i in part],
-                                             slots[j], microbatches, record_timing=record_timing)
-                             if part else None for j, part in enumerate(parts)]
-                    t0 = time.perf_counter()
-                    self.round_started = time.monotonic()
-                    try:
-                        results = self._run_rounds(specs)
-                    finally:
-                        self.round_started = None
-                    self.stats["busy_s"] += time.perf_counter() - t0
-                    self.last_round = results[0]
-                except Exception as e:
-                    self.healthy = False
-                    self.last_error = f"{type(e).__name__}: {e}"
-                    raise
-                finally:
-                    for j, sl in enumerate(slots):
-                        if sl:
-                            self.slot_pools[j].free(sl)
-                for part, res in zip(parts, results):
-                    if not part:
-                        continue
-                    toks = torch.cat([t.t() for t in res.tokens], 0)  # [n, steps]
-                    for row, i in enumerate(part):
-                        ids = toks[row, : params[i].max_new_tokens].tolist()
-                        if params[i].stop_at_eos and self.mcfg.eos_token_id in ids:
-                            ids = ids[: ids.index(self.mcfg.eos_token_id) + 1]
-                        outs[i] = ids
-                self.stats["rounds"] += 1
-        self.stats["requests"] += len(prompts)
-        self.stats["tokens"] += sum(len(o) for o in outs)
-        return outs
-
-    # ------------------------------------------------------------------
     # Compat single-shard forwards (reference /forward and /forward_b)
     # ------------------------------------------------------------------
-    def _local_forward_range(self, x, start_stage: int, end_stage: int, ids_len: int,
-                             all_logits: bool):
+    def forward_a(self, input_ids: List[int]) -> torch.Tensor:
+        """Stage-0 output for a full sequence (reference ShardA, server.py:77-86):
+        embeddings + this pipeline's first stage, on the compat KV slot."""
         from .batch import BatchMeta
 
-        slot = self.slots.alloc(1)
-        try:
-            out = x
-            for i in range(start_stage, end_stage):
-                st = self.stages[i]
-                meta = BatchMeta.build(slot, [0], [ids_len], st.device)
-                out = out.to(st.device)
-                if st.last:
-                    out = st.forward(meta, out, all_logits=all_logits)
-                else:
-                    out = st.forward(meta, out)
-            return out
-        finally:
-            self.slots.free(slot)
-
-    def forward_a(self, input_ids: List[int]) -> torch.Tensor:
-        """Stage-0 output for a full sequence (reference ShardA, server.py:77-86)."""
-        if self.mode != "local" or self.P < 2:
-            raise RuntimeError("forward_a needs a local engine with >= 2 stages")
-        ids = torch.tensor(input_ids, dtype=torch.int32, device=self.stages[0].device)
-        return self._local_forward_range(ids, 0, 1, len(input_ids), False)
+        if len(input_ids) > self.max_seq:
+            raise ValueError(f"sequence length {len(input_ids)} exceeds {self.max_seq}")
+        if self.P < 2:
+            raise RuntimeError("forward_a needs >= 2 pipeline stages")
+        st = self.stages[0]
+        with self._lock:
+            ids = torch.tensor(input_ids, dtype=torch.int32, device=st.device)
+            meta = BatchMeta.build([self.kv_slots + 1], [0], [len(input_ids)], st.device)
+            return st.forward(meta, ids)
 
     def forward_b(self, hidden: torch.Tensor) -> torch.Tensor:
-        """Remaining stages + ln_f + lm_head over all positions (ShardB, server.py:98-103)."""
-        if self.mode != "local" or self.P < 2:
-            raise RuntimeError("forward_b needs a local engine with >= 2 stages")
+        """Remaining stages + ln_f + lm_head over all positions (ShardB,
+        server.py:98-103).  Local: stage by stage in this process; dist: the
+        hidden rows travel stage 1 -> P-1 over the pipeline edges and the
+        logits come back on the return edge, between decode sessions."""
+        from .batch import BatchMeta
+
+        if self.P < 2:
+            raise RuntimeError("forward_b needs >= 2 pipeline stages")
         h = hidden.reshape(-1, self.mcfg.hidden).float()
-        out = self._local_forward_range(h, 1, self.P, h.shape[0], True)
-        return out[:, : self.mcfg.vocab_size]
+        T = h.shape[0]
+        if T > self.max_seq:
+            raise ValueError(f"sequence length {T} exceeds {self.max_seq}")
+        with self._lock:
+            if self.mode == "local":
+                out = h
+                for st in self.stages[1:]:
+                    meta = BatchMeta.build([self.kv_slots + 1], [0], [T], st.device)
+                    out = st.forward(meta, out.to(st.device), all_logits=st.last)
+                return out[:, : self.mcfg.vocab_size]
+            w0 = self.workers[0]
+            gp = GroupPlan(0, kind="fwd_b", fwd_rows=T)
+            plan = StepPlan(step=-2, groups=[gp])
+            for r in range(1, self.P):
+                self.plan_ch.send(r, plan)
+            for r in range(1, self.P):
+                self.plan_ch.send(r, StepPlan(step=-1, end=True))
+            dev = self.devices[0]
+            x = h.to(dev).contiguous()
+            self.transport.send(x, 1, "fwd").wait()
+            out = torch.empty(T, self.mcfg.vocab_padded, dtype=torch.float32, device=dev)
+            self.transport.irecv(out, self.P - 1, "ret").wait()
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            return out[:, : self.mcfg.vocab_size]
+
+
+def _with_index(dev: torch.device) -> torch.device:
+    if dev.type == "cuda" and dev.index is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return dev
 
 
 def _make_slot_allocator(n: int):

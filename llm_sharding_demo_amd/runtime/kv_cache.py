@@ -9,8 +9,10 @@ Layout (one allocation per stage):
     buf[layer, 0|1 (K|V), slot, kv_head, position, head_dim]   bf16 on GPU
 Each (slot, head) row-block is contiguous over positions, so the decode
 attention kernel streams K and V for one sequence/head as one linear 1 KiB-
-per-wave-instruction read.  Sized for MI355X's 288 GB HBM: `plan_slots`
-picks the slot count from the free-memory budget.
+per-wave-instruction read.  Sized for MI355X's 288 GB HBM: the engine asks
+`plan_slots` for the slot count that fits the free-memory budget after the
+stage's weights (runtime/engine.py `_kv_slots`, reported on /health and
+/metrics); two extra slots hold decode pad rows and compat forwards.
 """
 from __future__ import annotations
 
@@ -43,21 +45,27 @@ class KVCache:
 
 
 def plan_slots(requested: int, n_layers: int, n_kv: int, max_seq: int, head_dim: int,
-               device, fraction: float = 0.85, elt: int = 2) -> int:
-    """Largest slot count <= requested that fits `fraction` of free device memory."""
+               device, fraction: float = 0.85, elt: int = 2, reserve: int = 0,
+               mem_get_info=None) -> int:
+    """Largest slot count <= requested whose KV fits `fraction` of the free
+    device memory left after `reserve` bytes (the stage's weights, loaded
+    after this is decided).  `mem_get_info` is injectable for tests."""
     dev = torch.device(device)
-    if dev.type != "cuda":
+    if dev.type != "cuda" and mem_get_info is None:
         return requested
-    free, _ = torch.cuda.mem_get_info(dev)
+    free, _ = (mem_get_info or torch.cuda.mem_get_info)(dev)
     per = KVCache.bytes_per_slot(n_layers, n_kv, max_seq, head_dim, elt)
-    fit = int(free * fraction) // max(per, 1)
+    if per == 0:  # a stage without attention halves holds no KV
+        return requested
+    fit = int(max(0, free - reserve) * fraction) // per
     if fit < 1:
         raise MemoryError(f"KV cache: one slot needs {per / 2**30:.2f} GiB, free {free / 2**30:.2f} GiB")
     return min(requested, fit)
 
 
 class SlotAllocator:
-    """Host-side free list of KV slots (native version: csrc/runtime/scheduler.cpp)."""
+    """Host-side free list of KV slots (native version: SlotAllocator in
+    csrc/runtime/runtime.cpp)."""
 
     def __init__(self, n: int):
         self._free: List[int] = list(range(n - 1, -1, -1))

@@ -1,26 +1,31 @@
-"""Request scheduling in front of the pipeline engine: a batching request
-queue and a round watchdog.
+"""Iteration-level request scheduler (continuous batching) + round watchdog.
 
 Reference behaviour (`server.py:154-210`): every /generate
 runs its own decode loop in FastAPI's threadpool; concurrent requests share
 nothing and each pays the full per-token HTTP round trips (measured: 4
 concurrent requests -> 0.83 tok/s aggregate vs 0.69 for one).
 
-Here concurrent requests are coalesced into pipeline rounds:
+Here one scheduler (on the thread that drives pipeline stage 0) owns every
+sequence and decides, at every decode step, a `StepPlan` (runtime/plan.py)
+that all stages execute:
 
-* `RequestBatcher` -- one scheduler thread owns the engine; round formation
-  runs in the native `BatchQueue` (csrc/runtime/batch_queue.h, TSan-tested).  Callers enqueue a
-  request and block on its completion; the scheduler takes the first waiting
-  request, keeps collecting for up to `window_ms` (or until the engine's
-  batch capacity is reached), then runs ONE round for the whole group: every
-  request is a sequence of that round's microbatches, so the pipeline stages
-  see a full batch instead of B = 1 (quirk Q12).  Requests with very
-  different lengths are split into separate rounds (a round runs
-  max(max_new_tokens) steps for all its sequences).
-* `Watchdog` -- a per-round deadline: if a round (a hung
-  RCCL peer, a dead stage) runs past `round_timeout_s`, the engine is marked
-  unhealthy with a clear error, /health reports it, and the waiting requests
-  fail instead of hanging forever.
+  * requests wait in an admission queue (the native `BatchQueue`,
+    csrc/runtime/batch_queue.h) and JOIN a microbatch group at the next step
+    boundary when the group has a free row and the replica a free KV slot;
+    their prompts are prefilled by that step's item (chunked when
+    PREFILL_CHUNK is set), and the final chunk's sample is their first token;
+  * a sequence LEAVES its group at the step after its last token was
+    scheduled (max_new_tokens) or after its EOS was read back (stop_at_eos),
+    so a short request never waits behind a long one;
+  * decode rows are kept compacted and padded to a power-of-two bucket, so
+    the per-(group, bucket) hipGraphs stay valid across steps and requests;
+  * sampled token ids come back to the host asynchronously (D2H copy + event
+    per item); the scheduler runs at most a few steps ahead of the GPU.
+
+`Watchdog` puts a deadline on pipeline progress: if the
+engine makes no progress for `round_timeout_s` (a hung RCCL peer, a dead
+stage) it is marked unhealthy with a clear error and waiting requests fail
+instead of hanging forever.
 """
 from __future__ import annotations
 
@@ -30,9 +35,12 @@ import logging
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Callable, Deque, Dict, List, Optional
+
+import torch
 
 from ..config import SamplingParams
+from .plan import Chunk, GroupPlan, Row, StepPlan
 
 log = logging.getLogger("llm_sharding_demo_amd.scheduler")
 
@@ -46,7 +54,8 @@ class Request:
     prompt_ids: List[int]
     params: SamplingParams
     t_submit: float = field(default_factory=time.monotonic)
-    t_start: float = 0.0
+    t_start: float = 0.0        # joined the pipeline (prefill issued)
+    t_first: float = 0.0        # first token read back (TTFT = t_first - t_submit)
     t_done: float = 0.0
     output: Optional[List[int]] = None
     error: Optional[BaseException] = None
@@ -62,6 +71,11 @@ class Request:
     @property
     def done(self) -> bool:
         return self._done.is_set()
+
+    def finish(self, output=None, error=None) -> None:
+        self.output, self.error = output, error
+        self.t_done = time.monotonic()
+        self._done.set()
 
 
 class PyBatchQueue:
@@ -115,6 +129,19 @@ class PyBatchQueue:
             groups[-1].append(id_)
         return groups
 
+    def try_pop(self, k: int) -> List[int]:
+        """Up to k queued ids in FIFO order, without waiting."""
+        with self._cv:
+            out = []
+            while self._q and len(out) < k:
+                out.append(self._q.popleft()[0])
+            self.popped += len(out)
+            return out
+
+    def wait_nonempty(self, timeout_s: float) -> bool:
+        with self._cv:
+            return self._cv.wait_for(lambda: self._closed or self._q, timeout_s)
+
     def close(self) -> None:
         with self._cv:
             self._closed = True
@@ -143,105 +170,335 @@ def make_batch_queue(max_batch: int, length_ratio: float = 4.0, native: bool = T
         from .native import load
 
         R = load()
-        if R is not None and hasattr(R, "BatchQueue"):
+        if R is not None and hasattr(R, "BatchQueue") and hasattr(R.BatchQueue, "try_pop"):
             return R.BatchQueue(max_batch, length_ratio)
     return PyBatchQueue(max_batch, length_ratio)
 
 
-class RequestBatcher:
-    """Coalesce concurrent generate requests into pipeline rounds.  Round
-    formation (window, capacity, length groups) lives in the batch queue
-    (native BatchQueue); this class owns the request payloads by id."""
+# ---------------------------------------------------------------------------
+# Scheduler
+# ---------------------------------------------------------------------------
 
-    def __init__(self, engine, window_ms: float = 2.0, max_batch: Optional[int] = None,
-                 length_ratio: float = 4.0, native: bool = True):
-        self.engine = engine
-        self.window = window_ms / 1e3
-        # whole capacity of the engine: KV slots x pipeline replicas
-        cap = engine.slots.capacity * max(1, getattr(engine, "R", 1))
-        self.max_batch = min(max_batch or cap, cap)
-        self.length_ratio = length_ratio
-        self._nq = make_batch_queue(self.max_batch, length_ratio, native)
-        self._reqs: Dict[int, Request] = {}
-        self._lock = threading.Lock()
-        self._ids = itertools.count()
-        self.stats = {"batches": 0, "requests": 0, "max_batch_seen": 0}
-        self._thread = threading.Thread(target=self._loop, name="lsd-batcher", daemon=True)
-        self._thread.start()
+@dataclass
+class Seq:
+    id: int
+    req: Request
+    prompt: List[int]
+    params: SamplingParams
+    seed: int
+    rep: int = 0
+    g: int = -1
+    slot: int = -1
+    prefilled: int = 0          # prompt tokens whose chunks have been issued
+    issued: int = 0             # output tokens whose production has been issued
+    pos: int = 0                # next decode input position
+    sstep: int = 1              # sampler counter of the next decode draw
+    tokens: List[int] = field(default_factory=list)
+    stop: bool = False          # EOS read back (stop_at_eos): leave at the next step
+    left: bool = False
 
     @property
-    def native(self) -> bool:
-        return not isinstance(self._nq, PyBatchQueue)
+    def want(self) -> int:
+        return self.params.max_new_tokens
 
-    # ------------------------------------------------------------------
+
+@dataclass
+class Produced:
+    """Composition of one item that produced tokens: how to read its
+    token-return vector [decode rows (b) | final prefill chunks]."""
+    b: int
+    rows: List[int]             # seq ids of decode rows [0, n)
+    finals: List[int]           # seq ids whose final prefill chunk was sampled
+    release: List[int] = field(default_factory=list)  # seqs whose last item this was
+    step: int = 0
+
+
+@dataclass
+class GroupHost:
+    rows: List[int] = field(default_factory=list)
+    prefilling: List[int] = field(default_factory=list)
+    prev: Optional[Produced] = None
+
+
+def _bucket(n: int, cap: int) -> int:
+    if n <= 0:
+        return 0
+    b = 1
+    while b < n:
+        b <<= 1
+    return min(b, cap)
+
+
+class Scheduler:
+    """Continuous-batching scheduler for one engine (every pipeline replica).
+
+    Runs on the thread that drives stage 0 of replica 0.  `run_until()` is
+    the loop; `submit()` is thread-safe."""
+
+    def __init__(self, engine, groups: int, cap: int):
+        self.eng = engine
+        self.R = engine.R
+        self.M, self.cap = groups, cap
+        self.queue = make_batch_queue(max(1, cap * groups * self.R))
+        self._pending: Dict[int, Request] = {}
+        self._ids = itertools.count()
+        self._plock = threading.Lock()
+        self.seqs: Dict[int, Seq] = {}
+        self.waiting: Deque[int] = collections.deque()     # admitted to the scheduler, not yet joined
+        self.groups = [[GroupHost() for _ in range(groups)] for _ in range(self.R)]
+        self.step = 0
+        self.readouts: Deque[tuple] = collections.deque()  # (step, ready(), tokens(), Produced)
+        self.lock = threading.RLock()                       # one driver at a time
+        self.timing = False
+        self.step_log: List[tuple] = []                     # (step, had_prefill) of timed steps
+        self.stats = {"steps": 0, "joins": 0, "leaves": 0, "max_rows": 0, "captures": 0}
+        self.prefill_budget = engine.cfg.prefill_budget
+        self.chunk = engine.cfg.prefill_chunk
+        self._rng = engine._rng
+        self._expect: Dict[tuple, Produced] = {}   # (replica, step, group) -> item awaiting readout
+
+    # -- admission ---------------------------------------------------------
     def submit(self, prompt_ids: List[int], params: SamplingParams) -> Request:
-        if self._nq.closed:
-            raise RuntimeError("batcher is closed")
-        if not self.engine.healthy:  # fail fast: the scheduler may be stuck in a dead round
-            raise RuntimeError(f"engine unhealthy: {self.engine.last_error}")
-        params.validate()
-        req = Request(list(prompt_ids), params)
+        req = Request(list(map(int, prompt_ids)), params)
+        if params.max_new_tokens == 0:
+            req.finish([])
+            return req
         rid = next(self._ids)
-        with self._lock:
-            self._reqs[rid] = req
-        if not self._nq.push(rid, params.max_new_tokens):
-            with self._lock:
-                self._reqs.pop(rid, None)
-            raise RuntimeError("batcher is closed")
+        with self._plock:
+            self._pending[rid] = req
+        if not self.queue.push(rid, params.max_new_tokens):
+            with self._plock:
+                self._pending.pop(rid, None)
+            raise RuntimeError("scheduler is closed")
         return req
-
-    def generate(self, prompt_ids: List[int], params: SamplingParams,
-                 timeout: Optional[float] = None) -> List[int]:
-        return self.submit(prompt_ids, params).wait(timeout)
 
     @property
     def queue_depth(self) -> int:
-        return self._nq.depth
+        return self.queue.depth + len(self.waiting)
 
-    def close(self) -> None:
-        self._nq.close()
-        self._thread.join(timeout=5)
+    def _take_new(self) -> None:
+        ids = self.queue.try_pop(1 << 20)
+        with self._plock:
+            reqs = [(i, self._pending.pop(i)) for i in ids]
+        for i, req in reqs:
+            seed = req.params.seed if req.params.seed is not None else self._rng.getrandbits(62)
+            self.seqs[i] = Seq(i, req, req.prompt_ids, req.params, seed)
+            self.waiting.append(i)
 
-    # ------------------------------------------------------------------
-    def _take(self, ids: List[int]) -> List[Request]:
-        with self._lock:
-            return [self._reqs.pop(i) for i in ids]
+    def has_work(self) -> bool:
+        if self.waiting or self.queue.depth:
+            return True
+        for rep in self.groups:
+            for gh in rep:
+                if gh.rows or gh.prefilling or gh.prev is not None:
+                    return True
+        return False
 
-    def _loop(self) -> None:
-        while True:
-            groups = self._nq.next_groups(self.window)  # blocks (GIL released when native)
-            if not groups:
-                break  # closed
-            n = sum(len(g) for g in groups)
-            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], n)
-            for ids in groups:
-                group = self._take(ids)
-                t0 = time.monotonic()
-                for r in group:
-                    r.t_start = t0
+    # -- plan building ---------------------------------------------------------
+    def _admit(self, rep: int, gh_idx: int, room: int) -> List[int]:
+        pool = self.eng.slot_pools[rep]
+        out = []
+        while self.waiting and room > 0 and pool.available > 0:
+            sid = self.waiting.popleft()
+            s = self.seqs[sid]
+            s.rep, s.g = rep, gh_idx
+            s.slot = pool.alloc(1)[0]
+            s.req.t_start = time.monotonic()
+            out.append(sid)
+            room -= 1
+            self.stats["joins"] += 1
+        return out
+
+    def _group_plan(self, rep: int, g: int, step: int) -> Optional[GroupPlan]:
+        gh = self.groups[rep][g]
+        gp = GroupPlan(g)
+        prev = gh.prev
+        gh.prev = None
+        if prev is not None:
+            gp.ret = prev.b + len(prev.finals)
+        # leaves: every token scheduled, or EOS read back
+        keep = []
+        for sid in gh.rows:
+            s = self.seqs[sid]
+            if s.issued >= s.want or s.stop:
+                s.left = True
+                self.stats["leaves"] += 1
+                if prev is not None:
+                    prev.release.append(sid)
+            else:
+                keep.append(sid)
+        act = list(prev.finals) if prev is not None else []
+        new_rows = keep + act
+        changed = new_rows != gh.rows
+        # joins (capacity counts rows + sequences still prefilling)
+        room = self.cap - len(new_rows) - len(gh.prefilling)
+        gh.prefilling += self._admit(rep, g, room)
+        # prefill chunks (FIFO, one chunk per sequence per step, token budget)
+        budget = self.prefill_budget or (1 << 62)
+        chunks, finals = [], []
+        for sid in list(gh.prefilling):
+            s = self.seqs[sid]
+            L = len(s.prompt)
+            n = L - s.prefilled if self.chunk <= 0 else min(self.chunk, L - s.prefilled)
+            if chunks and n > budget:
+                break
+            budget -= n
+            a = s.prefilled
+            final = a + n == L
+            p = s.params
+            chunks.append(Chunk(sid, s.slot, a, s.prompt[a:a + n], final, p.temperature, p.top_k,
+                                p.greedy, s.seed))
+            s.prefilled += n
+            if final:
+                gh.prefilling.remove(sid)
+                finals.append(sid)
+                s.issued = 1
+                s.pos = L
+                s.sstep = 1
+        gp.chunks = chunks
+        # decode rows
+        gp.n = len(new_rows)
+        gp.b = _bucket(gp.n, self.cap)
+        if changed:
+            old_index = {sid: i for i, sid in enumerate(gh.rows)}
+            rows = []
+            for j, sid in enumerate(new_rows):
+                s = self.seqs[sid]
+                src = old_index[sid] if sid in old_index else prev.b + prev.finals.index(sid)
+                p = s.params
+                rows.append(Row(sid, s.slot, s.pos, p.temperature, p.top_k, p.greedy, s.seed,
+                                s.sstep, src))
+            gp.rows = rows
+        if gp.n:
+            top = max(self.seqs[sid].pos for sid in new_rows) + 1
+            gp.ctxb = min(-(-top // 256) * 256, self.eng.max_seq)
+            for sid in new_rows:  # this step issues one token per decode row
+                s = self.seqs[sid]
+                s.issued += 1
+                s.pos += 1
+                s.sstep += 1
+        gh.rows = new_rows
+        self.stats["max_rows"] = max(self.stats["max_rows"], gp.n)
+        if gp.b or finals:
+            gh.prev = Produced(gp.b, list(new_rows), finals, step=step)
+        if prev is not None:
+            self._register(rep, step, g, prev)
+        if not (gp.ret or gp.has_work):
+            return None
+        return gp
+
+    def _register(self, rep: int, step: int, g: int, prod: Produced) -> None:
+        self._expect[(rep, step, g)] = prod
+
+    def build_step(self) -> Optional[List[StepPlan]]:
+        """Plans of the next step for every replica, or None when idle."""
+        self._take_new()
+        if not self.has_work():
+            return None
+        s = self.step
+        self.step += 1
+        plans = []
+        for rep in range(self.R):
+            gps = [gp for g in range(self.M) for gp in [self._group_plan(rep, g, s)] if gp is not None]
+            plans.append(StepPlan(step=s, groups=gps, replica=rep, timing=self.timing))
+        self.stats["steps"] += 1
+        if self.timing:
+            self.step_log.append((s, any(gp.chunks for p in plans for gp in p.groups)))
+        return plans
+
+    # -- token readout -----------------------------------------------------------
+    def on_readout(self, plan: StepPlan, gp: GroupPlan, ret: torch.Tensor) -> None:
+        """Stage-0 worker callback: the token-return vector of group gp.g's
+        previous item is in `ret` (in stream order): copy it to the host."""
+        prod = self._expect.pop((plan.replica, plan.step, gp.g))
+        n = gp.ret
+        if ret.is_cuda:
+            host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+            host.copy_(ret[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self.readouts.append((plan.step, ev.query, ev.synchronize, host, prod))
+        else:
+            host = ret[:n].clone()
+            self.readouts.append((plan.step, lambda: True, lambda: None, host, prod))
+
+    def push_remote_readout(self, step: int, tokens: List[int], prod_key) -> None:
+        """Replica > 0 readouts arrive over the control plane (dist + DP)."""
+        rep, st, g = prod_key
+        prod = self._expect.pop((rep, st, g))
+        host = torch.tensor(tokens, dtype=torch.int32)
+        self.readouts.append((step, lambda: True, lambda: None, host, prod))
+
+    def poll(self, block_until_step: Optional[int] = None) -> None:
+        """Process completed readouts (in order).  With block_until_step,
+        wait for every readout of steps <= that one."""
+        while self.readouts:
+            step, ready, sync, host, prod = self.readouts[0]
+            if not ready():
+                if block_until_step is None or step > block_until_step:
+                    return
+                sync()
+            self.readouts.popleft()
+            self._assign(host, prod)
+
+    def _assign(self, host: torch.Tensor, prod: Produced) -> None:
+        toks = host.tolist()
+        eos = self.eng.mcfg.eos_token_id
+        now = time.monotonic()
+        for i, sid in enumerate(prod.rows):
+            self._give(self.seqs.get(sid), toks[i], eos, now)
+        for j, sid in enumerate(prod.finals):
+            self._give(self.seqs.get(sid), toks[prod.b + j], eos, now)
+        for sid in prod.release:
+            self._release(sid)
+
+    def _give(self, s: Optional[Seq], tok: int, eos: int, now: float) -> None:
+        if s is None or s.req.done or len(s.tokens) >= s.want:
+            return
+        if not s.tokens:
+            s.req.t_first = now
+        s.tokens.append(tok)
+        if s.params.stop_at_eos and tok == eos:
+            s.stop = True
+        if len(s.tokens) >= s.want or s.stop:
+            s.req.finish(list(s.tokens))
+
+    def _release(self, sid: int) -> None:
+        s = self.seqs.pop(sid, None)
+        if s is None:
+            return
+        if s.slot >= 0:
+            self.eng.slot_pools[s.rep].free([s.slot])
+        if not s.req.done:
+            s.req.finish(list(s.tokens))
+
+    # -- failure -----------------------------------------------------------------
+    def fail_all(self, err: BaseException) -> None:
+        for s in list(self.seqs.values()):
+            if not s.req.done:
+                s.req.finish(error=err)
+            if s.slot >= 0:
                 try:
-                    outs = self.engine.generate_ids([r.prompt_ids for r in group],
-                                                     [r.params for r in group], record_timing=True)
-                    for r, o in zip(group, outs):
-                        r.output = o
-                except BaseException as e:  # fail the whole group, keep serving
-                    log.error("round failed: %s", e)
-                    for r in group:
-                        r.error = e
-                t1 = time.monotonic()
-                for r in group:
-                    r.t_done = t1
-                    r._done.set()
-                self.stats["batches"] += 1
-                self.stats["requests"] += len(group)
-        # fail whatever is still queued
-        for r in self._take(self._nq.drain()):
-            r.error = RuntimeError("batcher closed")
-            r._done.set()
+                    self.eng.slot_pools[s.rep].free([s.slot])
+                except Exception:  # pragma: no cover
+                    pass
+        self.seqs.clear()
+        self.waiting.clear()
+        self.readouts.clear()
+        self._expect.clear()
+        with self._plock:
+            pend = list(self._pending.values())
+            self._pending.clear()
+        for rid in self.queue.drain():
+            pass
+        for req in pend:
+            req.finish(error=err)
+        self.groups = [[GroupHost() for _ in range(self.M)] for _ in range(self.R)]
+
 
 
 class Watchdog:
-    """Marks the engine unhealthy when a round outlives its deadline."""
+    """Marks the engine unhealthy when the pipeline stops making progress."""
 
     def __init__(self, engine, round_timeout_s: float, poll_s: float = 0.25):
         self.engine = engine
@@ -260,7 +517,7 @@ class Watchdog:
             elapsed = time.monotonic() - started
             if elapsed > self.timeout:
                 self.fired = True
-                msg = f"round exceeded its {self.timeout:.0f} s deadline (running {elapsed:.0f} s)"
+                msg = f"no pipeline progress for {elapsed:.0f} s (deadline {self.timeout:.0f} s)"
                 log.error("watchdog: %s; marking engine unhealthy", msg)
                 self.engine.healthy = False
                 self.engine.last_error = f"WatchdogTimeout: {msg}"

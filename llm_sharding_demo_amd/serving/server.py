@@ -17,9 +17,11 @@ Roles (env SHARD_ROLE, `server.py:21`):
 Additions: optional sampling fields on /generate (temperature, top_k, greedy,
 seed, stop_at_eos; defaults = reference sampler), 422 on empty/over-long
 prompts (instead of the reference's 500, quirk Q9), GET /health, GET /metrics
-(Prometheus text).  Concurrent /generate calls are batched into shared
-pipeline rounds by runtime/scheduler.py's RequestBatcher; a round watchdog
-turns a hung pipeline into 503s instead of hanging requests.
+(Prometheus text).  Concurrent /generate calls are batched at decode-step
+granularity by the engine's continuous-batching scheduler
+(runtime/scheduler.py): a request joins the running batch at the next step
+and leaves as soon as it has its tokens; a progress watchdog turns a hung
+pipeline into 503s instead of hanging requests.
 """
 from __future__ import annotations
 
@@ -98,13 +100,13 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
     metrics = Metrics()
     app = FastAPI(title="llm-sharding-demo (MI355X)")
     app.state.engine, app.state.shard, app.state.metrics = engine, shard, metrics
-    batcher = watchdog = None
+    watchdog = None
     if engine is not None:
-        from ..runtime.scheduler import RequestBatcher, Watchdog
+        from ..runtime.scheduler import Watchdog
 
-        batcher = RequestBatcher(engine, window_ms=cfg.batch_window_ms)
+        engine.start_loop()
         watchdog = Watchdog(engine, cfg.round_timeout_s)
-    app.state.batcher, app.state.watchdog = batcher, watchdog
+    app.state.watchdog = watchdog
 
     def _role_is(*roles):
         return role in roles or role == "all"
@@ -123,6 +125,8 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
                 h = engine.forward_a(req.input_ids)
         except ValueError as e:
             raise HTTPException(422, str(e))
+        except RuntimeError as e:  # e.g. a single-stage engine has no shard A / B split
+            raise HTTPException(400, str(e))
         return {"hidden_states": h.float().cpu().unsqueeze(0).tolist()}
 
     @app.post("/forward_b")
@@ -143,6 +147,8 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
                 outs.append(lg.float().cpu())
         except ValueError as e:
             raise HTTPException(422, str(e))
+        except RuntimeError as e:
+            raise HTTPException(400, str(e))
         return {"logits": torch.stack(outs).tolist()}
 
     @app.post("/generate")
@@ -166,9 +172,13 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
                 if len(ids) + sp.max_new_tokens > engine.max_seq:
                     raise ValueError(f"prompt ({len(ids)}) + max_new_tokens ({sp.max_new_tokens}) "
                                      f"exceeds the context limit {engine.max_seq}")
-                out = batcher.generate(ids, sp, timeout=cfg.request_timeout_s)
+                req_ = engine.submit(ids, sp)
+                out = req_.wait(timeout=cfg.request_timeout_s)
+                metrics.observe_request(len(out), time.perf_counter() - t0,
+                                        ttft_s=(req_.t_first - req_.t_submit) if req_.t_first else None)
             else:
                 out = http_generate(cfg, ids, sp)
+                metrics.observe_request(len(out), time.perf_counter() - t0)
         except ValueError as e:
             raise HTTPException(422, str(e))
         except RequestTimeout as e:
@@ -177,10 +187,6 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
             if engine is not None and not engine.healthy:
                 raise HTTPException(503, f"engine unhealthy: {engine.last_error}")
             raise
-        dt = time.perf_counter() - t0
-        metrics.observe_request(len(out), dt)
-        if engine is not None and engine.last_round is not None and engine.last_round.step_times_ms:
-            metrics.observe_steps(engine.last_round.step_times_ms)
         return {"generated": tok.decode(ids + out, skip_special_tokens=True)}
 
     @app.get("/health")
@@ -189,7 +195,7 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
         body = {"status": "ok" if ok else "unhealthy", "role": role, "model": mc.name}
         if engine is not None:
             body.update(stages=engine.P, plan=engine.plan, unit_plan=engine.unit_plan, mode=engine.mode,
-                        devices=[str(d) for d in engine.devices])
+                        devices=[str(d) for d in engine.devices], **engine.kv_info())
             if not ok:
                 body["error"] = engine.last_error
         if shard is not None:
@@ -199,22 +205,30 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
 
     @app.get("/metrics", response_class=PlainTextResponse)
     def prom():
-        extra = {}
+        gauges, counters = {}, {}
         if engine is not None:
-            extra = {"engine_healthy": 1 if engine.healthy else 0,
-                     "engine_stages": engine.P,
-                     "kv_slots_free": engine.slots.available,
-                     "kv_slots_total": engine.slots.capacity,
-                     "queue_depth": batcher.queue_depth,
-                     "batched_rounds_total": batcher.stats["batches"],
-                     "batched_requests_total": batcher.stats["requests"],
-                     "max_batch_seen": batcher.stats["max_batch_seen"]}
-            lr = engine.last_round
-            for st in (lr.stages if lr is not None else []):
-                tag = f"stage{st['stage']}" + (f"_replica{st['replica']}" if st.get("replica") else "")
-                extra[f"{tag}_busy_fraction"] = st["busy_fraction"]
-                extra[f"{tag}_bubble_fraction"] = 1.0 - st["busy_fraction"]
-        return metrics.render(extra)
+            sch = engine.scheduler
+            kv = engine.kv_info()
+            gauges = {"engine_healthy": 1 if engine.healthy else 0,
+                      "engine_stages": engine.P,
+                      "kv_slots_free": kv["kv_slots_free"],
+                      "kv_slots_total": kv["kv_slots"] * engine.R,
+                      "kv_cache_bytes_stage0": kv["kv_bytes_stage0"],
+                      "queue_depth": sch.queue_depth,
+                      "max_batch_rows_seen": sch.stats["max_rows"]}
+            counters = {"pipeline_steps_total": sch.stats["steps"],
+                        "sequence_joins_total": sch.stats["joins"],
+                        "sequence_leaves_total": sch.stats["leaves"],
+                        "hipgraph_captures_total": sum(w.captures for w in engine.workers)}
+            ls = engine.last_session
+            if ls is not None:
+                if ls.step_times_ms:
+                    metrics.observe_steps(ls.step_times_ms, key=id(ls))
+                for st in ls.stages:
+                    tag = f"stage{st['stage']}" + (f"_replica{st['replica']}" if st.get("replica") else "")
+                    gauges[f"{tag}_busy_fraction"] = st["busy_fraction"]
+                    gauges[f"{tag}_bubble_fraction"] = 1.0 - st["busy_fraction"]
+        return metrics.render(gauges, counters)
 
     return app
 

@@ -156,7 +156,7 @@ def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp):
             out = eng.generate_ids({PROMPTS!r}, SamplingParams(greedy=True, max_new_tokens=6))
             out2 = eng.generate_ids({PROMPTS!r}[:2], SamplingParams(greedy=True, max_new_tokens=6),
                                     record_timing=True)
-            stages = eng.last_round.stages
+            stages = eng.last_session.stages
             assert sorted(st["stage"] for st in stages) == sorted(list(range(eng.P)) * {dp}), stages
             eng.shutdown()
             print("RESULT", json.dumps([out, out2]))
@@ -265,6 +265,6 @@ def test_stage_busy_stats_local_and_gloo():
     eng = Engine(EngineConfig(model_id="gpt2-test", num_stages=3, max_batch=8, device="cpu"))
     eng.generate_ids(PROMPTS, SamplingParams(greedy=True, max_new_tokens=4), microbatches=3,
                      record_timing=True)
-    st = eng.last_round.stages
+    st = eng.last_session.stages
     assert [s["stage"] for s in st] == [0, 1, 2]
     assert all(0.0 < s["busy_fraction"] <= 1.0 and s["items"] > 0 for s in st)

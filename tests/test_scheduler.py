@@ -1,10 +1,13 @@
-"""Request batching + round watchdog (runtime/scheduler.py), CPU.
+"""Continuous (iteration-level) batching + progress watchdog
+(runtime/scheduler.py, runtime/engine.py), CPU.
 
-Reference behaviour: concurrent /generate calls run
-independent decode loops, and a dead shard shows up only as a 30 s HTTP
-timeout per hop.  Here concurrent requests must share pipeline rounds with
-outputs identical to running them alone, and a hung round must flip /health
-and fail requests fast.
+Reference behaviour (`server.py:154-155`): concurrent
+/generate calls run independent decode loops, so a short request never waits
+for a long one, and a dead shard shows up only as a 30 s HTTP timeout per hop.
+Here concurrent requests share pipeline steps with outputs identical to
+running them alone, a request joins a running batch at the next decode step
+and leaves when it has its tokens, and a stalled pipeline flips /health and
+fails requests fast.
 """
 import threading
 import time
@@ -13,35 +16,58 @@ import pytest
 
 from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
 from llm_sharding_demo_amd.runtime.engine import Engine
-from llm_sharding_demo_amd.runtime.scheduler import RequestBatcher, RequestTimeout, Watchdog
+from llm_sharding_demo_amd.runtime.scheduler import RequestTimeout, Watchdog
 
 PROMPTS = [[5, 6, 7, 8], [11], [300, 2, 9], [1, 2], [40, 41, 42, 43, 44], [9, 9], [3], [77, 1]]
 
 
-def _engine(P=2, max_batch=8):
-    return Engine(EngineConfig(model_id="gpt2-test", num_stages=P, max_batch=max_batch, device="cpu"))
+def _engine(P=2, max_batch=8, **kw):
+    return Engine(EngineConfig(model_id="gpt2-test", num_stages=P, max_batch=max_batch,
+                               device="cpu", **kw))
 
 
-def test_concurrent_requests_share_rounds_and_match_solo():
+def test_concurrent_requests_share_steps_and_match_solo():
     sp = SamplingParams(greedy=True, max_new_tokens=5)
     solo = _engine().generate_ids(PROMPTS, sp)
     eng = _engine()
-    b = RequestBatcher(eng, window_ms=200)
+    eng.start_loop()
     outs = [None] * len(PROMPTS)
 
     def go(i):
-        outs[i] = b.generate(PROMPTS[i], SamplingParams(greedy=True, max_new_tokens=5), timeout=60)
+        outs[i] = eng.submit(PROMPTS[i], SamplingParams(greedy=True, max_new_tokens=5)).wait(60)
 
     ts = [threading.Thread(target=go, args=(i,)) for i in range(len(PROMPTS))]
     for t in ts:
         t.start()
     for t in ts:
         t.join()
-    b.close()
+    eng.stop_loop()
     assert outs == solo
-    assert b.stats["requests"] == len(PROMPTS)
-    assert b.stats["batches"] < len(PROMPTS)  # requests were coalesced
+    st = eng.scheduler.stats
+    assert st["joins"] == len(PROMPTS) and st["leaves"] == len(PROMPTS)
+    assert st["max_rows"] > 1  # requests decoded side by side
     assert eng.slots.available == eng.slots.capacity
+    eng.shutdown()
+
+
+def test_short_request_joins_running_batch_and_finishes_first():
+    """A 2-token request submitted while a 500-token generation is running
+    joins at the next step boundary and completes long before it."""
+    eng = _engine(P=2, max_batch=4, max_seq_len=1024)
+    eng.start_loop()
+    long = eng.submit([1, 2, 3], SamplingParams(greedy=True, max_new_tokens=500))
+    while eng.scheduler.stats["steps"] < 20:  # the long one is decoding
+        time.sleep(0.005)
+    short = eng.submit([7, 8], SamplingParams(greedy=True, max_new_tokens=2))
+    assert len(short.wait(60)) == 2
+    assert not long.done  # still generating when the short one finished
+    assert len(long.wait(120)) == 500
+    assert short.t_done < long.t_done
+    # the short one reused nothing of the long one's output: same as alone
+    assert short.output == _engine(P=1).generate_ids([[7, 8]], SamplingParams(greedy=True,
+                                                                              max_new_tokens=2))[0]
+    eng.stop_loop()
+    eng.shutdown()
 
 
 def test_seeded_sampling_independent_of_batching():
@@ -49,75 +75,70 @@ def test_seeded_sampling_independent_of_batching():
           for i in range(len(PROMPTS))]
     solo = [_engine(P=1).generate_ids([p], [s])[0] for p, s in zip(PROMPTS, sp)]
     eng = _engine()
-    b = RequestBatcher(eng, window_ms=200)
-    reqs = [b.submit(p, s) for p, s in zip(PROMPTS, sp)]
+    eng.start_loop()
+    reqs = []
+    for p, s in zip(PROMPTS, sp):  # staggered arrivals: different batch compositions
+        reqs.append(eng.submit(p, s))
+        time.sleep(0.002)
     outs = [r.wait(60) for r in reqs]
-    b.close()
+    eng.stop_loop()
     assert outs == solo
 
 
-def test_length_groups_and_more_requests_than_slots():
+def test_more_requests_than_slots_and_mixed_lengths():
     eng = _engine(max_batch=3)
-    b = RequestBatcher(eng, window_ms=200)
     lens = [1, 2, 16, 3, 20, 1, 2]
-    reqs = [b.submit([1 + i, 2], SamplingParams(greedy=True, max_new_tokens=n)) for i, n in enumerate(lens)]
-    outs = [r.wait(60) for r in reqs]
-    b.close()
+    ps = [SamplingParams(greedy=True, max_new_tokens=n) for n in lens]
+    outs = eng.generate_ids([[1 + i, 2] for i in range(len(lens))], ps)
     assert [len(o) for o in outs] == lens
-    # a 1-token request never waits for the 20-token round
-    assert reqs[0].t_done <= reqs[4].t_done
+    assert eng.slots.available == eng.slots.capacity
 
 
-def test_round_error_fails_group_not_batcher():
+def test_eos_stop_leaves_early():
+    eng = _engine(P=1)
+    base = eng.generate_ids([[5, 6]], SamplingParams(greedy=True, max_new_tokens=12))[0]
+    eos = base[3]
+    eng.mcfg = type(eng.mcfg)(**{**eng.mcfg.__dict__, "eos_token_id": eos})
+    out = eng.generate_ids([[5, 6]], SamplingParams(greedy=True, max_new_tokens=12,
+                                                    stop_at_eos=True))[0]
+    assert out == base[: base.index(eos) + 1]
+    assert eng.slots.available == eng.slots.capacity
+
+
+def test_bad_request_does_not_hurt_engine():
     eng = _engine()
-    b = RequestBatcher(eng, window_ms=50)
+    eng.start_loop()
     with pytest.raises(ValueError):
-        b.generate([], SamplingParams(greedy=True, max_new_tokens=2), timeout=30)
-    eng.healthy = True  # a bad request is not an engine fault
-    eng.last_error = None
-    assert len(b.generate([1, 2], SamplingParams(greedy=True, max_new_tokens=2), timeout=30)) == 2
-    b.close()
-
-
-class _SlowEngine:
-    """Stand-in whose round hangs (a dead RCCL peer)."""
-
-    def __init__(self):
-        self.healthy, self.last_error, self.round_started = True, None, None
-        self.R = 1
-        self.slots = type("S", (), {"capacity": 4})()
-        self.release = threading.Event()
-
-    def generate_ids(self, prompts, params, **kw):
-        self.round_started = time.monotonic()
-        self.release.wait(30)
-        self.round_started = None
-        return [[0] for _ in prompts]
+        eng.submit([], SamplingParams(greedy=True, max_new_tokens=2))
+    assert eng.healthy
+    assert len(eng.submit([1, 2], SamplingParams(greedy=True, max_new_tokens=2)).wait(30)) == 2
+    eng.stop_loop()
 
 
 def test_watchdog_marks_unhealthy_and_requests_fail_fast():
-    eng = _SlowEngine()
+    def fault(edge, src, dst, seq):
+        return 1.5 if seq >= 2 else None  # the link stalls after two messages
+
+    eng = Engine(EngineConfig(model_id="gpt2-test", num_stages=2, max_batch=4, device="cpu"),
+                 fault=fault)
     wd = Watchdog(eng, round_timeout_s=0.3, poll_s=0.05)
-    b = RequestBatcher(eng, window_ms=1)
-    req = b.submit([1], SamplingParams(greedy=True, max_new_tokens=1))
-    with pytest.raises(RequestTimeout):
-        req.wait(timeout=0.8)
-    assert not eng.healthy and "deadline" in eng.last_error and wd.fired
+    eng.start_loop()
+    req = eng.submit([1], SamplingParams(greedy=True, max_new_tokens=20))
+    with pytest.raises((RequestTimeout, RuntimeError)):
+        req.wait(timeout=10)
+    assert not eng.healthy and "progress" in eng.last_error and wd.fired
     with pytest.raises(RuntimeError, match="unhealthy"):
-        b.submit([2], SamplingParams(greedy=True, max_new_tokens=1))
-    eng.release.set()
-    assert req.wait(5) == [0]
-    b.close()
+        eng.submit([2], SamplingParams(greedy=True, max_new_tokens=1))
     wd.close()
 
 
-def test_http_concurrent_generate_batched():
+def test_http_concurrent_generate_and_metrics():
     from fastapi.testclient import TestClient
 
     from llm_sharding_demo_amd.serving.server import create_app
 
     cfg = EngineConfig(model_id="gpt2-test", num_stages=2, max_batch=8, device="cpu",
-                       batch_window_ms=200)
+                       metrics_every=1)
     eng = Engine(cfg)
     app = create_app(cfg, engine=eng)
     client = TestClient(app)
@@ -134,6 +155,25 @@ def test_http_concurrent_generate_batched():
         t.join()
     assert all("generated" in r and r["generated"].startswith(f"hi {i}") for i, r in enumerate(res))
     m = client.get("/metrics").text
-    assert "llmshard_batched_requests_total 6" in m
+    assert "# TYPE llmshard_requests_total counter" in m and "llmshard_requests_total 6" in m
+    assert "llmshard_output_tokens_total 24" in m
+    assert "llmshard_sequence_joins_total 6" in m
     assert "llmshard_stage1_busy_fraction" in m and "llmshard_token_latency_p50_ms" in m
-    assert app.state.batcher.stats["batches"] < 6
+    assert "llmshard_time_to_first_token_p50_s" in m
+    h = client.get("/health").json()
+    assert h["kv_slots"] == 8 and h["status"] == "ok"
+    eng.stop_loop()
+
+
+def test_metrics_throughput_is_wall_clock():
+    """N concurrent requests finishing together: tok/s is tokens over the
+    wall-clock span, not over the summed request latencies."""
+    from llm_sharding_demo_amd.utils.metrics import Metrics
+
+    m = Metrics()
+    t0 = time.monotonic()
+    time.sleep(0.2)
+    for _ in range(4):  # 4 overlapping requests of 0.2 s, 10 tokens each
+        m.observe_request(10, time.monotonic() - t0)
+    tps = m.tokens_per_second()
+    assert 120 < tps < 220, tps  # ~40 tokens / 0.2 s, not 40 / 0.8 s
