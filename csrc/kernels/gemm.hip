@@ -1020,9 +1020,10 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
   }
   const int tn = (p.N + TBN - 1) / TBN;
   dim3 grid(tm * tn * p.splits), block(256);
-  // the cap counts 128x64 tiles: a 128x128 ring grid gets half as many
-  // workgroups (vocab-wide lm_head grids stay on the 2-blocks/CU kernel)
-  const int cap128 = g_ring_tn == 64 ? g_tiled3_max_blocks / 2 : g_tiled3_max_blocks;
+  // the cap counts 128x64 tiles whatever LSD_RING_TN says: a 128x128 ring
+  // grid gets half as many workgroups (vocab-wide lm_head grids stay on the
+  // 2-blocks/CU kernel; profiles/r1_ab_ring_n64.log)
+  const int cap128 = g_tiled3_max_blocks / 2;
   if (tm * tn * p.splits <= cap128 && g_ring_slots == 4)
     hipLaunchKernelGGL((gemm_ring_kernel<EPI, 4, 128>), grid, block, 0, st, p, tm, tn);
   else if (tm * tn * p.splits <= cap128)

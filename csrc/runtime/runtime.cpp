@@ -7,19 +7,13 @@
 //
 //   * SlotAllocator   -- KV-cache slot free list (each slot = one sequence's
 //                        [layers][2][heads][max_seq][hd] region on every stage).
-//   * split_even      -- microbatch boundaries for a round.
 //   * partition_minmax-- exact min-max contiguous layer partition (DP), the
 //                        cost model lives in Python (parallel/partition.py).
-//   * simulate_pipeline -- discrete-event model of the static per-stage
-//                        schedule (parallel/pipeline.py): proves every send has
-//                        a matching receive in FIFO order per edge (deadlock
-//                        freedom) and returns the makespan / bubble fraction
-//                        for given stage and link costs.
-//   * percentile      -- latency statistics for /metrics and bench.
-//   * BatchQueue      -- the serving scheduler's request queue (batch_queue.h):
-//                        thread-safe push from HTTP threads, window/length-group
-//                        round formation for the one scheduler thread (GIL
-//                        released while it waits).
+//   * BatchQueue      -- the serving scheduler's admission queue (batch_queue.h):
+//                        thread-safe push from HTTP threads; the continuous-
+//                        batching scheduler drains it at every decode step
+//                        (try_pop); window/length-group round formation
+//                        (next_groups) for batch jobs.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -70,13 +64,6 @@ class SlotAllocator {
   std::vector<int> free_;
 };
 
-std::vector<int> split_even(int n, int m) {
-  if (m < 1) throw std::invalid_argument("m >= 1");
-  std::vector<int> b(m + 1);
-  for (int i = 0; i <= m; ++i) b[i] = (int)std::llround((double)i * n / m);
-  return b;
-}
-
 // costs[i] = cost of layer i; head = extra cost of the last stage.
 std::vector<std::pair<int, int>> partition_minmax(const std::vector<double>& costs, int P,
                                                   double head) {
@@ -106,55 +93,6 @@ std::vector<std::pair<int, int>> partition_minmax(const std::vector<double>& cos
   return plan;
 }
 
-// Simulate the static schedule of parallel/pipeline.py.  stage_cost[r] = time
-// of one microbatch forward on stage r; link = one-hop latency.  Receives are
-// matched FIFO per directed edge; a stage blocks only on its own next input.
-py::dict simulate_pipeline(int P, int M, int G, const std::vector<double>& stage_cost,
-                           double link) {
-  if ((int)stage_cost.size() != P) throw std::invalid_argument("stage_cost must have P entries");
-  // arrival time of the input of item (s, m) at stage r
-  std::map<std::tuple<int, int, int>, double> arrive;
-  std::vector<double> free_at(P, 0.0);
-  std::vector<double> busy(P, 0.0);
-  // Process items in schedule order per stage; because every dependency
-  // points to an earlier (stage, item) in the global topological order
-  // (s, m, r), iterating in that order resolves all inputs.
-  double makespan = 0;
-  for (int s = 0; s < G; ++s)
-    for (int m = 0; m < M; ++m)
-      for (int r = 0; r < P; ++r) {
-        double ready;
-        if (r == 0)
-          ready = (s == 0) ? 0.0 : arrive.at({0, s, m});
-        else
-          ready = arrive.at({r, s, m});
-        double start = std::max(ready, free_at[r]);
-        double end = start + stage_cost[r];
-        free_at[r] = end;
-        busy[r] += stage_cost[r];
-        makespan = std::max(makespan, end);
-        if (r + 1 < P)
-          arrive[{r + 1, s, m}] = end + link;
-        else if (s + 1 < G)
-          arrive[{0, s + 1, m}] = end + (P > 1 ? link : 0.0);
-      }
-  double bubble = 0;
-  for (int r = 0; r < P; ++r) bubble += 1.0 - busy[r] / makespan;
-  py::dict d;
-  d["makespan"] = makespan;
-  d["bubble_fraction"] = bubble / P;
-  d["tokens_per_time"] = (double)M * G / makespan;
-  return d;
-}
-
-double percentile(std::vector<double> xs, double q) {
-  if (xs.empty()) return 0.0;
-  std::sort(xs.begin(), xs.end());
-  double k = (xs.size() - 1) * q;
-  size_t lo = (size_t)k, hi = std::min(lo + 1, xs.size() - 1);
-  return xs[lo] + (xs[hi] - xs[lo]) * (k - lo);
-}
-
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "native host runtime for llm_sharding_demo_amd";
   py::class_<SlotAllocator>(m, "SlotAllocator")
@@ -163,11 +101,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def("free", &SlotAllocator::free)
       .def_property_readonly("available", &SlotAllocator::available)
       .def_property_readonly("capacity", &SlotAllocator::capacity);
-  m.def("split_even", &split_even);
   m.def("partition_minmax", &partition_minmax);
-  m.def("simulate_pipeline", &simulate_pipeline, py::arg("P"), py::arg("M"), py::arg("G"),
-        py::arg("stage_cost"), py::arg("link") = 0.0);
-  m.def("percentile", &percentile);
   using lsd_rt::BatchQueue;
   py::class_<BatchQueue>(m, "BatchQueue")
       .def(py::init<int, double>(), py::arg("max_batch"), py::arg("length_ratio") = 4.0)

@@ -517,7 +517,8 @@ class StageWorker:
         meta = BatchMeta.build([self.compat_slot], [0], [T], self.device)
         x = ins[0]
         if self.last:
-            out = st.forward(meta, x, all_logits=True)
+            # only the real vocabulary crosses (the HIP lm_head pads it)
+            out = st.forward(meta, x, all_logits=True)[:, : st.cfg.vocab_size].contiguous()
             self.send_pending.setdefault(gp.g, []).append(self.t.send(out, 0, "ret"))
         else:
             out = st.forward(meta, x)

@@ -562,7 +562,8 @@ class Engine:
 
         if self.P < 2:
             raise RuntimeError("forward_b needs >= 2 pipeline stages")
-        h = hidden.reshape(-1, self.mcfg.hidden).float()
+        # a stage updates its input rows in place (the residual stream): copy
+        h = hidden.reshape(-1, self.mcfg.hidden).float().clone()
         T = h.shape[0]
         if T > self.max_seq:
             raise ValueError(f"sequence length {T} exceeds {self.max_seq}")
@@ -583,11 +584,11 @@ class Engine:
             dev = self.devices[0]
             x = h.to(dev).contiguous()
             self.transport.send(x, 1, "fwd").wait()
-            out = torch.empty(T, self.mcfg.vocab_padded, dtype=torch.float32, device=dev)
+            out = torch.empty(T, self.mcfg.vocab_size, dtype=torch.float32, device=dev)
             self.transport.irecv(out, self.P - 1, "ret").wait()
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
-            return out[:, : self.mcfg.vocab_size]
+            return out
 
 
 def _with_index(dev: torch.device) -> torch.device:

@@ -45,17 +45,6 @@ def test_slot_allocator(R):
     a.free(s)
     with pytest.raises(RuntimeError):
         a.free([0])  # double free detected
-    assert R.split_even(10, 3) == [0, 3, 7, 10]
-
-
-def test_schedule_simulation(R):
-    one = R.simulate_pipeline(1, 1, 50, [1.0], 0.0)
-    assert abs(one["tokens_per_time"] - 1.0) < 1e-9
-    # M >= P microbatches keep a balanced pipeline busy; M < P leaves bubbles
-    full = R.simulate_pipeline(4, 8, 50, [1.0] * 4, 0.05)
-    starved = R.simulate_pipeline(4, 2, 50, [1.0] * 4, 0.05)
-    assert full["bubble_fraction"] < 0.1 < starved["bubble_fraction"]
-    assert full["tokens_per_time"] > 3 * starved["tokens_per_time"] / 2
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
@@ -82,8 +71,11 @@ def test_runtime_under_asan_ubsan(tmp_path):
         for _ in range(200):
             s = a.alloc(7); a.free(s)
         R.partition_minmax([1.0] * 48, 8, 2.6)
-        R.simulate_pipeline(8, 16, 64, [1.0] * 8, 0.1)
-        print(R.percentile([3.0, 1.0, 2.0], 0.5))
+        q = R.BatchQueue(8, 4.0)
+        for i in range(20):
+            q.push(i, 1 + i % 5)
+        got = q.try_pop(5) + [x for g in q.next_groups(0.0) for x in g]
+        print(len(got), float(sorted(got)[2]))
     """))
     env = dict(os.environ, LD_PRELOAD=libasan, ASAN_OPTIONS="detect_leaks=0",
                UBSAN_OPTIONS="halt_on_error=1")

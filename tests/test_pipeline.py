@@ -175,6 +175,47 @@ def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp):
     assert out2 == golden[:2]
 
 
+def test_gloo_compat_forwards_in_dist_mode(tmp_path):
+    """/forward and /forward_b served by a torchrun engine (role `all`): stage
+    0's output on rank 0, the rest of the pipeline over the pipeline edges;
+    equal to the in-process 2-stage engine."""
+    script = tmp_path / "w.py"
+    script.write_text(textwrap.dedent(f"""
+        import sys, json, torch
+        sys.path.insert(0, {ROOT!r})
+        from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
+        from llm_sharding_demo_amd.runtime.engine import Engine, build_engine
+        cfg = EngineConfig(model_id="gpt2-test", max_batch=4, device="cpu", transport="gloo")
+        eng = build_engine(cfg)
+        if eng.rank != 0:
+            eng.worker_loop()
+        else:
+            ids = [5, 6, 7, 8, 9]
+            h = eng.forward_a(ids)
+            lg = eng.forward_b(h)
+            out = eng.generate_ids([ids], SamplingParams(greedy=True, max_new_tokens=3))
+            lg2 = eng.forward_b(h)  # again, after a decode session
+            loc = Engine(cfg.replace(num_stages=2, transport="auto"))
+            hl = loc.forward_a(ids)
+            ll = loc.forward_b(hl)
+            print("RESULT", json.dumps([float((h - hl).abs().max()), float((lg - ll).abs().max()),
+                                        float((lg2 - ll).abs().max()), list(lg.shape), out]))
+            eng.shutdown()
+    """))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={env['MASTER_PORT']}", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")][0]
+    dh, dl, dl2, shape, out = json.loads(line[len("RESULT "):])
+    assert dh == 0.0 and dl == 0.0 and dl2 == 0.0
+    assert shape == [5, 1000] and len(out[0]) == 3
+
+
 # ---------------------------------------------------------------------------
 # Half-layer (unit) partitioning: a stage boundary between a layer's attention
 # and MLP halves must reproduce the unsplit model exactly.
