@@ -163,7 +163,14 @@ def main() -> int:
                        "sampler": "greedy" if args.greedy else "T0.6/top-k40",
                        "hipgraphs": not args.no_graphs},
         }
+        if args.loopback_stages and eng.last_session is not None:
+            out["stage_busy"] = [st["busy_fraction"] for st in eng.last_session.stages]
         print(json.dumps(out), flush=True)
+        hp = getattr(eng, "_hostprof", None)
+        if hp is not None and hp[3]:
+            print(f"host per decode step: plan {hp[0] / hp[3] * 1e6:.1f} us, issue {hp[1] / hp[3] * 1e6:.1f} us "
+                  f"({hp[1] / max(hp[4], 1) * 1e6:.1f} us per item), readout wait "
+                  f"{hp[2] / hp[3] * 1e6:.1f} us over {hp[3]} steps", file=sys.stderr)
     if N > 1:
         if rank == 0:
             eng.shutdown()  # stop the followers, barrier, tear the groups down in order

@@ -365,11 +365,14 @@ class LoopbackTransport(Transport):
         fabric = self.fabric
 
         def post():
+            from .pipeline import GPU_GATE
+
             buf, ev = fabric.get(key, f"stage {self.rank} waiting on {edge} from stage {src}")
-            cur = torch.cuda.current_stream(out.device)
-            cur.wait_event(ev)
-            buf.record_stream(cur)  # the sender's pool must not recycle it early
-            out.copy_(buf, non_blocking=True)
+            with GPU_GATE.shared():  # never beside another stage thread's capture
+                cur = torch.cuda.current_stream(out.device)
+                cur.wait_event(ev)
+                buf.record_stream(cur)  # the sender's pool must not recycle it early
+                out.copy_(buf, non_blocking=True)
 
         return Handle(out, None, post=post)
 

@@ -44,7 +44,52 @@ from ..runtime.plan import GroupPlan, StepPlan
 from ..utils.tracing import trace_range
 from .comm import Handle, SendHandle, Transport
 
-_CAPTURE_LOCK = threading.Lock()
+class _CaptureGate:
+    """Stage threads sharing one GPU (local mode) issue work concurrently, but
+    HIP rejects a stream capture that overlaps another thread's stream
+    operations (hipErrorStreamCaptureIsolation) or a replay during a capture.
+    Every GPU-issuing section holds the gate shared; a capture holds it
+    exclusively.  Blocking transport waits happen outside the gate, so a
+    stage waiting for its input never holds up a capture.  One thread per
+    process (dist, P = 1): always uncontended."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._readers = 0
+        self._writer = False
+        self._waiting = 0
+
+    @contextlib.contextmanager
+    def shared(self):
+        with self._cv:
+            while self._writer or self._waiting:
+                self._cv.wait()
+            self._readers += 1
+        try:
+            yield
+        finally:
+            with self._cv:
+                self._readers -= 1
+                if self._readers == 0:
+                    self._cv.notify_all()
+
+    @contextlib.contextmanager
+    def exclusive(self):
+        with self._cv:
+            self._waiting += 1
+            while self._writer or self._readers:
+                self._cv.wait()
+            self._waiting -= 1
+            self._writer = True
+        try:
+            yield
+        finally:
+            with self._cv:
+                self._writer = False
+                self._cv.notify_all()
+
+
+GPU_GATE = _CaptureGate()
 
 
 def prefill_chunks(lens: List[int], chunk: int) -> List[Tuple[List[int], List[int]]]:
@@ -203,9 +248,6 @@ class StageWorker:
         self.H = stage.cfg.hidden
         self.scratch_slot, self.compat_slot = scratch_slot, compat_slot
         self.use_graphs = True
-        # Each stage worker owns a non-blocking stream: no device-wide syncs, so
-        # one stage may capture a hipGraph while another (same GPU) keeps running.
-        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         # Group "lanes": group g of this stage runs on lanes[g % L], so
         # independent groups overlap on the GPU -- one's latency-bound
         # phases (small GEMMs, split-K tails) run beside another's bandwidth-
@@ -223,6 +265,7 @@ class StageWorker:
         self.last_stats: Optional[dict] = None
         self.step_events: List[tuple] = []   # stage 0: (step, event) at each step start
         self.readout = None        # stage 0: callable(step, plan, ret_tensor) for token readout
+        self._tls = threading.local()
 
     # ------------------------------------------------------------------
     def configure(self, groups: int, cap: int) -> None:
@@ -245,8 +288,6 @@ class StageWorker:
             self.send_pending.clear()
             for lane in self.lanes:
                 lane.synchronize()
-            if self.stream is not None:
-                self.stream.synchronize()
 
     # ------------------------------------------------------------------
     # timing
@@ -261,16 +302,46 @@ class StageWorker:
         return self.last_stats
 
     # ------------------------------------------------------------------
+    def begin_session(self) -> None:
+        """Order the lanes behind the caller's stream once per session.  Steps
+        inside a session add no cross-stream hops: group g always runs on
+        lanes[g % L], so its items are ordered by the lane itself (a per-step
+        lane <-> stream event round trip costs ~0.2 ms of GPU idle)."""
+        if not self.lanes:
+            return
+        with self._gpu():
+            cur = torch.cuda.current_stream(self.device)
+            for lane in self.lanes:
+                lane.wait_stream(cur)
+
+    def end_session(self) -> None:
+        if not self.lanes:
+            return
+        with self._gpu():
+            cur = torch.cuda.current_stream(self.device)
+            for lane in self.lanes:
+                cur.wait_stream(lane)
+
     def run_step(self, plan: StepPlan, nxt: Optional[StepPlan] = None) -> None:
-        """Execute this stage's part of one step.  `nxt` (the following step's
-        plan, when already known) lets the last item post the next step's
-        first receive ahead of its compute."""
-        if self.stream is None:
-            return self._run_step(plan, nxt)
-        self.stream.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self.stream):
-            self._run_step(plan, nxt)
-        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        """Execute this stage's part of one step (between begin_session and
+        end_session).  `nxt` (the following step's plan, when already known)
+        lets the last item post the next step's first receive ahead of its
+        compute."""
+        items = self._items(plan)
+        following = self._items(nxt)
+        L = max(1, len(self.lanes))
+        self.stage.backend.concurrency = max(1, min(L, sum(1 for gp in items if gp.has_work)))
+        if self.first and plan.timing and self.device.type == "cuda":
+            with self._gpu(), self.on_lane(0):
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+            self.step_events.append((plan.step, ev))
+        if items:
+            self._post(items[0])
+        for i, gp in enumerate(items):
+            nx = items[i + 1] if i + 1 < len(items) else (following[0] if following else None)
+            with self.on_lane(gp.g), trace_range(f"stage{self.r}/step{plan.step}/g{gp.g}"):
+                self._item(plan, gp, nx)
 
     def _items(self, plan: Optional[StepPlan]) -> List[GroupPlan]:
         if plan is None or plan.end or plan.stop:
@@ -281,27 +352,6 @@ class StageWorker:
         if gp.kind == "fwd_b":
             return self.r > 0
         return gp.has_work or (self.first and gp.ret > 0)
-
-    def _run_step(self, plan: StepPlan, nxt: Optional[StepPlan]) -> None:
-        items = self._items(plan)
-        following = self._items(nxt)
-        L = max(1, len(self.lanes))
-        for lane in self.lanes:
-            lane.wait_stream(torch.cuda.current_stream(self.device))
-        self.stage.backend.concurrency = max(1, min(L, sum(1 for gp in items if gp.has_work)))
-        if self.first and plan.timing and self.device.type == "cuda":
-            with self.on_lane(0):
-                ev = torch.cuda.Event(enable_timing=True)
-                ev.record()
-            self.step_events.append((plan.step, ev))
-        if items:
-            self._post(items[0])
-        for i, gp in enumerate(items):
-            nx = items[i + 1] if i + 1 < len(items) else (following[0] if following else None)
-            with self.on_lane(gp.g), trace_range(f"stage{self.r}/step{plan.step}/g{gp.g}"):
-                self._item(plan, gp, nx)
-        for lane in self.lanes:
-            torch.cuda.current_stream(self.device).wait_stream(lane)
 
     # ------------------------------------------------------------------
     # receives
@@ -372,13 +422,14 @@ class StageWorker:
         # outputs of this group's previous item must have left before we overwrite them
         for h in self.send_pending.pop(gp.g, []):
             h.wait()
-        mark = self.stats.mark() if (self.stats is not None and plan.timing) else None
-        if gp.kind == "fwd_b":
-            self._fwd_b(gp, ins)
-        else:
-            self._step_item(plan, gp, gs, ins)
-        if mark is not None:
-            self.stats.marks.append((mark, self.stats.mark()))
+        with self._gpu():
+            mark = self.stats.mark() if (self.stats is not None and plan.timing) else None
+            if gp.kind == "fwd_b":
+                self._fwd_b(gp, ins)
+            else:
+                self._step_item(plan, gp, gs, ins)
+            if mark is not None:
+                self.stats.marks.append((mark, self.stats.mark()))
         if not early:
             self._post(nx)
 
@@ -497,7 +548,7 @@ class StageWorker:
             return body()
         if key in gs.graphs:
             g, out = gs.graphs[key]
-            g.replay()
+            g.replay()  # inside the item's shared section of GPU_GATE
             return out
         if key not in gs.seen:  # first use: eager (allocates workspaces outside capture)
             gs.seen.add(key)
@@ -534,7 +585,7 @@ class StageWorker:
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        with _CAPTURE_LOCK:
+        with self._gate_released(), GPU_GATE.exclusive():
             with torch.cuda.stream(s):
                 g.capture_begin(capture_error_mode="thread_local")
                 try:
@@ -543,6 +594,37 @@ class StageWorker:
                     g.capture_end()
         torch.cuda.current_stream(self.device).wait_stream(s)
         return g, out
+
+    @contextlib.contextmanager
+    def _gate_released(self):
+        """Drop this thread's shared hold on GPU_GATE (held by the item being
+        executed) around an exclusive section, and take it back after."""
+        held = getattr(self._tls, "shared", None)
+        if held is None:
+            yield
+            return
+        held.__exit__(None, None, None)
+        try:
+            yield
+        finally:
+            cm = GPU_GATE.shared()
+            cm.__enter__()
+            self._tls.shared = cm
+
+    @contextlib.contextmanager
+    def _gpu(self):
+        """Shared hold on GPU_GATE for a GPU-issuing section of this thread."""
+        if self.device.type != "cuda":
+            yield
+            return
+        cm = GPU_GATE.shared()
+        cm.__enter__()
+        self._tls.shared = cm
+        try:
+            yield
+        finally:
+            self._tls.shared.__exit__(None, None, None)
+            self._tls.shared = None
 
 
 def _h2d(vals, dtype, dev) -> torch.Tensor:

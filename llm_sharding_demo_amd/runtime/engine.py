@@ -98,6 +98,8 @@ class Engine:
         self.loop_thread: Optional[threading.Thread] = None
         self._stop_loop = threading.Event()
         self._wake = threading.Event()  # a request was submitted (serving loop)
+        # LSD_HOST_PROFILE=1: host seconds in (plan, issue, readout wait), steps
+        self._hostprof = [0.0, 0.0, 0.0, 0, 0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
         self.kv_slots = 0
 
         if mode == "local":
@@ -311,22 +313,35 @@ class Engine:
             sch.step_log.clear()
             self._start_stats()
         lag = self.P + 2  # steps the host may run ahead of the GPU readouts
+        hp = self._hostprof
         ran = False
         try:
             cur = sch.build_step()
             if cur is not None:
                 ran = True
                 self._send_plans(cur)
+                w0.begin_session()
             while cur is not None:
                 self._check_followers()
                 if not self.healthy:
                     raise RuntimeError(self.last_error)
-                self.round_started = time.monotonic()
+                self.round_started = t0 = time.monotonic()
                 nxt = sch.build_step()
                 self._send_plans(nxt)
+                t1 = time.monotonic()
                 w0.run_step(cur[0], nxt[0] if nxt is not None else None)
+                t2 = time.monotonic()
                 sch.poll(block_until_step=cur[0].step - lag)
+                if hp is not None and not any(gp.chunks for gp in cur[0].groups):
+                    t3 = time.monotonic()  # decode steps only (prefill issue is eager)
+                    hp[0] += t1 - t0
+                    hp[1] += t2 - t1
+                    hp[2] += t3 - t2
+                    hp[3] += 1
+                    hp[4] += sum(1 for gp in cur[0].groups if gp.has_work)
                 cur = nxt
+            if ran:
+                w0.end_session()
             # everything issued: wait for the outstanding readouts
             while sch.readouts or not until():
                 if sch.readouts:
@@ -358,9 +373,12 @@ class Engine:
         self.workers[0].start_stats()
 
     def _finish_stats(self) -> None:
+        from ..parallel.pipeline import GPU_GATE
+
         w0 = self.workers[0]
         if self.devices[0].type == "cuda":
-            torch.cuda.synchronize(self.devices[0])
+            with GPU_GATE.shared():
+                torch.cuda.synchronize(self.devices[0])
         stats = [w0.end_stats()]
         if self.mode == "local":
             for _ in range(self.P - 1):
@@ -385,13 +403,19 @@ class Engine:
         """Execute plans until the session ends (True) or stop (False)."""
         cur = recv()
         started = False
+        began = False
         while True:
-            if cur.stop:
-                return False
-            if cur.end:
+            if cur.stop or cur.end:
+                if began:
+                    worker.end_session()
+                if cur.stop:
+                    return False
                 if started or cur.timing:
                     self._follower_stats(worker, cur)
                 return True
+            if not began:
+                worker.begin_session()
+                began = True
             if cur.timing and not started:
                 worker.start_stats()
                 started = True
