@@ -33,7 +33,7 @@ class StageModel:
                  last: bool, device="cpu", dtype: Optional[torch.dtype] = None, seed: int = 0,
                  weights_path: Optional[str] = None, max_slots: int = 8, max_seq: int = 1024,
                  weights: Optional[Dict[str, torch.Tensor]] = None,
-                 units: Optional[Tuple[int, int]] = None):
+                 units: Optional[Tuple[int, int]] = None, backend=None):
         self.cfg = cfg
         self.device = torch.device(device)
         if dtype is None:
@@ -61,7 +61,9 @@ class StageModel:
         self.max_seq = min(max_seq, cfg.max_positions)
         self.kv = KVCache(len(self.kv_layers), max_slots, cfg.n_kv_heads, self.max_seq,
                           cfg.head_dim, dtype, self.device)
-        self.backend = get_backend(self.device)
+        # `backend` overrides the device default: the fp32 golden model runs the
+        # plain PyTorch ops (ops/reference.py) on the GPU (utils/golden.py)
+        self.backend = backend if backend is not None else get_backend(self.device)
         self.backend.prepare_stage(self)
 
     def _owns(self, name: str) -> bool:
