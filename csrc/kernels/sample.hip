@@ -9,6 +9,9 @@
 // loads (the row -- 200 KB for GPT-2, 500 KB for Llama-3 -- stays L2-resident
 // across passes).
 //   greedy: block argmax (lowest index on ties).
+//   top-k <= 64: threshold = k-th largest of 64 segment maxima (a lower bound
+//           of the k-th largest logit), filter pass, sort the ~100 candidates;
+//           a GPT-2 row is read from HBM once (both passes from registers).
 //   top-k : radix select of the k-th largest order-preserving key in three
 //           passes over bits [31:20], [19:8], [7:0] (4096/4096/256 bins; the
 //           exponent-heavy top bits are spread over 4096 bins so LDS atomics
@@ -128,6 +131,74 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
   }
 
   const int k = min(max(topk[row], 1), min(SMAX, V));
+  // ---- fast path (k <= 64): threshold from segment maxima, then filter.
+  // The 64 segments are the 16-thread groups of the row visit; the k-th
+  // largest segment maximum tau is <= the k-th largest logit (the top-k
+  // segment maxima are k distinct elements >= tau), so {x >= tau} holds the
+  // top k.  One pass for the maxima + one filter pass (the row stays in L2),
+  // ~100 candidates on real or random logits; the exact (value desc, index
+  // asc) order comes from the bitonic sort below, so the result equals the
+  // radix path's.  More than SMAX candidates (flat logits) -> radix path.
+  bool fast = k <= 64;
+  if (fast) {
+    // a row of <= CH * NT * 4 floats (GPT-2's) is loaded ONCE and both passes
+    // run from registers; longer rows (Llama-3's) re-read through L2
+    const bool one = V <= CH * NT * 4;
+    const int last = ((V - 1) >> 2) << 2;
+    f32x4 q[CH];
+    if (one) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        q[i] = *reinterpret_cast<const f32x4*>(x + min((tid + i * NT) * 4, last));
+    }
+    auto visit = [&](auto&& f) {
+      if (one) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int b = (tid + i * NT) * 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (b + j < V) f(q[i][j], b + j);
+        }
+      } else {
+        for_row(x, V, f);
+      }
+    };
+    float mx = -INFINITY;
+    visit([&](float val, int) { mx = fmaxf(mx, val); });
+    mx = fmaxf(mx, wave_xchg<1>(mx));
+    mx = fmaxf(mx, wave_xchg<2>(mx));
+    mx = fmaxf(mx, wave_xchg<4>(mx));
+    mx = fmaxf(mx, wave_xchg<8>(mx));
+    if ((tid & 15) == 0) cval[tid >> 4] = mx;
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    if (tid < 64) {
+      const float v = cval[tid];
+      int rank = 0;
+      for (int j = 0; j < 64; ++j) {
+        const float o = cval[j];
+        rank += (o > v || (o == v && j < tid)) ? 1 : 0;
+      }
+      if (rank == k - 1) redv[0] = v;
+    }
+    __syncthreads();
+    const float tau = redv[0];
+    __syncthreads();  // cval is reused for the candidates
+    visit([&](float val, int idx) {
+      if (val >= tau) {
+        const unsigned slot = atomicAdd(&s_cnt, 1u);
+        if (slot < SMAX) {
+          cval[slot] = val;
+          cidx[slot] = idx;
+        }
+      }
+    });
+    __syncthreads();
+    fast = s_cnt <= SMAX;  // uniform
+  }
+  const int nsel = fast ? (int)s_cnt : k;  // entries to sort (k winners on the radix path)
+  if (!fast) {
   // ---- radix select over 12 + 12 + 8 bits
   unsigned prefix = 0, mask = 0, need = k;
   const int shifts[3] = {20, 8, 0};
@@ -201,10 +272,11 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
       __syncthreads();
     }
   }
-  // ---- bitonic sort of the k winners: (value desc, index asc); pad to pow2
+  }  // radix path
+  // ---- bitonic sort of the winners / candidates: (value desc, index asc); pad to pow2
   int n2 = 1;
-  while (n2 < k) n2 <<= 1;
-  for (int i = k + tid; i < n2; i += NT) { cval[i] = -INFINITY; cidx[i] = 0x7fffffff; }
+  while (n2 < nsel) n2 <<= 1;
+  for (int i = nsel + tid; i < n2; i += NT) { cval[i] = -INFINITY; cidx[i] = 0x7fffffff; }
   __syncthreads();
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {

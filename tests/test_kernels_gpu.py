@@ -378,3 +378,31 @@ def test_sampler(C):
     for r in range(B):
         k = 1 if greedy[r] else int(topk[r])
         assert int(out[r]) in set(torch.topk(logits[r, :V], k).indices.tolist())
+
+
+@pytest.mark.parametrize("case", ["random", "ties", "flat", "quantized", "llama_vocab"])
+def test_sampler_fast_path_and_ties(C, case):
+    """top-k <= 64 takes the threshold/filter path; flat logits (more
+    candidates than fit) fall back to the radix path; ties are broken by the
+    lowest index in both -- bit-equal to the host reference either way."""
+    from llm_sharding_demo_amd.runtime.batch import counter_uniform
+
+    B, V, Vp = (12, 128256, 128256) if case == "llama_vocab" else (12, 50257, 50304)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    logits = torch.randn(B, Vp, device=DEV, generator=g) * 2
+    if case == "ties":  # many exact duplicates around the top
+        logits = (logits * 4).round() / 4
+    elif case == "flat":
+        logits[:6] = 0.25
+    elif case == "quantized":
+        logits = (logits * 16).round() / 16
+    logits[:, V:] = 100.0
+    temp = torch.linspace(0.5, 1.5, B, device=DEV)
+    topk = torch.tensor([1, 2, 5, 16, 40, 63, 64, 65, 40, 40, 200, 40], dtype=torch.int32, device=DEV)
+    greedy = torch.tensor([0] * 11 + [1], dtype=torch.int32, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 104729 + 11
+    step = torch.arange(B, dtype=torch.int64, device=DEV)
+    out = C.sample(logits, V, temp, topk, greedy, seeds, step)
+    exp = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), greedy.cpu(),
+                     counter_uniform(seeds.cpu(), step.cpu()), V)
+    assert out.cpu().tolist() == exp.tolist()

@@ -414,8 +414,9 @@ def main():
             bench_norm(64, H, s)
             bench_norm(128, H, s)
     if "sample" in which:
-        for g in (True, False):
-            bench_sample(64, 50257, g)
+        for B in (1, 64, 256):
+            for g in (True, False):
+                bench_sample(B, 50257, g)
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/microbench.json", "w") as f:
         json.dump(RESULTS, f, indent=1)
