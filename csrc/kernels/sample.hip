@@ -108,7 +108,13 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
   const int row = blockIdx.x, tid = threadIdx.x;
   const float* x = logits + (long)row * ld;
 
-  if (greedy[row]) {
+  // per-row parameters up front: their loads overlap the row read instead of
+  // adding a dependent round trip at the end
+  const int is_greedy = greedy[row];
+  const int k_req = topk[row];
+  const float T = temp[row];
+  const long long seed_r = seeds[row], step_r = step[row];
+  if (is_greedy) {
     float best = -INFINITY;
     int bi = 0x7fffffff;
     for_row(x, V, [&](float val, int idx) {
@@ -130,7 +136,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     return;
   }
 
-  const int k = min(max(topk[row], 1), min(SMAX, V));
+  const int k = min(max(k_req, 1), min(SMAX, V));
   // ---- fast path (k <= 64): threshold from segment maxima, then filter.
   // The 64 segments are the 16-thread groups of the row visit; the k-th
   // largest segment maximum tau is <= the k-th largest logit (the top-k
@@ -141,31 +147,31 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
   // radix path's.  More than SMAX candidates (flat logits) -> radix path.
   bool fast = k <= 64;
   if (fast) {
-    // a row of <= CH * NT * 4 floats (GPT-2's) is loaded ONCE and both passes
-    // run from registers; longer rows (Llama-3's) re-read through L2
+    // a row of <= CH * NT * 4 floats (GPT-2's) is loaded ONCE and every pass
+    // runs from registers (the tail past V masked to -inf at load time, so
+    // no per-element bounds checks); longer rows (Llama-3's) re-read via L2
     const bool one = V <= CH * NT * 4;
     const int last = ((V - 1) >> 2) << 2;
     f32x4 q[CH];
+    float mx = -INFINITY;
     if (one) {
 #pragma unroll
       for (int i = 0; i < CH; ++i)
         q[i] = *reinterpret_cast<const f32x4*>(x + min((tid + i * NT) * 4, last));
-    }
-    auto visit = [&](auto&& f) {
-      if (one) {
 #pragma unroll
-        for (int i = 0; i < CH; ++i) {
-          const int b = (tid + i * NT) * 4;
+      for (int i = 0; i < CH; ++i) {
+        const int b = (tid + i * NT) * 4;
+        if (b + 3 >= V) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (b + j < V) f(q[i][j], b + j);
+            if (b + j >= V) q[i][j] = -INFINITY;
         }
-      } else {
-        for_row(x, V, f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, q[i][j]);
       }
-    };
-    float mx = -INFINITY;
-    visit([&](float val, int) { mx = fmaxf(mx, val); });
+    } else {
+      for_row(x, V, [&](float val, int) { mx = fmaxf(mx, val); });
+    }
     mx = fmaxf(mx, wave_xchg<1>(mx));
     mx = fmaxf(mx, wave_xchg<2>(mx));
     mx = fmaxf(mx, wave_xchg<4>(mx));
@@ -173,27 +179,64 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     if ((tid & 15) == 0) cval[tid >> 4] = mx;
     if (tid == 0) s_cnt = 0;
     __syncthreads();
-    if (tid < 64) {
-      const float v = cval[tid];
+    if (tid < 64) {  // rank of segment `tid` among the 64 maxima (ties by segment)
+      const float sv = cval[tid];
       int rank = 0;
-      for (int j = 0; j < 64; ++j) {
-        const float o = cval[j];
-        rank += (o > v || (o == v && j < tid)) ? 1 : 0;
+#pragma unroll
+      for (int j4 = 0; j4 < 16; ++j4) {
+        const f32x4 o = reinterpret_cast<const f32x4*>(cval)[j4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rank += (o[e] > sv || (o[e] == sv && 4 * j4 + e < tid)) ? 1 : 0;
       }
-      if (rank == k - 1) redv[0] = v;
+      if (rank == k - 1) redv[0] = sv;
     }
     __syncthreads();
     const float tau = redv[0];
-    __syncthreads();  // cval is reused for the candidates
-    visit([&](float val, int idx) {
-      if (val >= tau) {
-        const unsigned slot = atomicAdd(&s_cnt, 1u);
+    const int lane = lane_id();
+    // compaction without per-element atomics: per-thread candidate count (and
+    // bit mask of register positions), wave scan, one LDS atomic per wave
+    int cnt = 0;
+    unsigned long long msk = 0;
+    if (one) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) msk |= q[i][j] >= tau ? (1ull << (4 * i + j)) : 0ull;
+      cnt = __popcll(msk);
+    } else {
+      for_row(x, V, [&](float val, int) { cnt += val >= tau ? 1 : 0; });
+    }
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    unsigned base = 0;
+    if (lane == 63) base = atomicAdd(&s_cnt, (unsigned)incl);
+    unsigned slot = __shfl(base, 63, 64) + (unsigned)(incl - cnt);
+    if (one) {
+      while (msk) {  // ~0-2 trips per thread; the value comes back from L2
+        const int e = __builtin_ctzll(msk);
+        msk &= msk - 1;
+        const int idx = (tid + (e >> 2) * NT) * 4 + (e & 3);
         if (slot < SMAX) {
-          cval[slot] = val;
+          cval[slot] = x[idx];
           cidx[slot] = idx;
         }
+        ++slot;
       }
-    });
+    } else {
+      for_row(x, V, [&](float val, int idx) {
+        if (val >= tau) {
+          if (slot < SMAX) {
+            cval[slot] = val;
+            cidx[slot] = idx;
+          }
+          ++slot;
+        }
+      });
+    }
     __syncthreads();
     fast = s_cnt <= SMAX;  // uniform
   }
@@ -273,6 +316,66 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     }
   }
   }  // radix path
+  // ---- <= 128 entries (fast-path candidates, or k <= 128 radix winners): wave 0 sorts them in
+  // registers (2 per lane, element e = 2 * lane + r, cross-lane steps by
+  // shuffles) and draws without another block barrier.
+  if (nsel <= 128) {
+    if (tid >= 64) return;
+    const int e0 = 2 * tid;
+    float v[2];
+    int ix[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const bool ok = e0 + r < nsel;
+      v[r] = ok ? cval[e0 + r] : -INFINITY;
+      ix[r] = ok ? cidx[e0 + r] : 0x7fffffff;
+    }
+#pragma unroll
+    for (int size = 2; size <= 128; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        if (stride == 1) {
+          const bool up = (e0 & size) == 0;
+          const bool first = v[0] > v[1] || (v[0] == v[1] && ix[0] < ix[1]);
+          if (up != first) {
+            const float tv = v[0]; v[0] = v[1]; v[1] = tv;
+            const int ti = ix[0]; ix[0] = ix[1]; ix[1] = ti;
+          }
+        } else {
+          const int pl = stride >> 1;  // partner lane = lane ^ pl, same r
+          const bool lower = (tid & pl) == 0;
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const bool up = ((e0 + r) & size) == 0;
+            const float pv = shfl_xor(v[r], pl);
+            const int pi = shfl_xor(ix[r], pl);
+            const bool own_first = v[r] > pv || (v[r] == pv && ix[r] < pi);
+            if (lower ? (own_first != up) : (own_first == up)) { v[r] = pv; ix[r] = pi; }
+          }
+        }
+      }
+    }
+    const float x0 = __shfl(v[0], 0, 64) / T;
+    const float u = counter_uniform(seed_r, step_r);
+    const float p0 = e0 < k ? __expf(v[0] / T - x0) : 0.f;
+    const float p1 = e0 + 1 < k ? __expf(v[1] / T - x0) : 0.f;
+    const float target = u * wave_sum(p0 + p1);
+    float pre = p0 + p1;  // inclusive prefix of the lane pairs
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const float o = __shfl_up(pre, d, 64);
+      if (tid >= d) pre += o;
+    }
+    const float c1 = pre, c0 = pre - p1;
+    const unsigned long long h0 = __ballot(e0 < k && c0 >= target);
+    const unsigned long long h1 = __ballot(e0 + 1 < k && c1 >= target);
+    int pick = k - 1;
+    const int l0 = h0 ? __builtin_ctzll(h0) : 64, l1 = h1 ? __builtin_ctzll(h1) : 64;
+    if (l0 < 64 || l1 < 64) pick = l0 <= l1 ? 2 * l0 : 2 * l1 + 1;
+    const int win = __shfl(pick & 1 ? ix[1] : ix[0], pick >> 1, 64);
+    if (tid == 0) out[row] = win;
+    return;
+  }
   // ---- bitonic sort of the winners / candidates: (value desc, index asc); pad to pow2
   int n2 = 1;
   while (n2 < nsel) n2 <<= 1;
@@ -295,10 +398,9 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
   }
   // ---- softmax over value/T and inverse-CDF draw (one wave, k <= 1024)
   if (tid < 64) {
-    const float T = temp[row];
     const float x0 = cval[0] / T;
     // running CDF in chunks of 64: lane l owns element base + l
-    const float u = counter_uniform(seeds[row], step[row]);
+    const float u = counter_uniform(seed_r, step_r);
     float tot = 0.f;
     for (int base = 0; base < k; base += 64) {
       const int i = base + tid;
