@@ -19,6 +19,8 @@ using lsd::GemvParams;
 extern "C" {
 hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws, hipStream_t st);
 void lsd_gemm_set_big_min(int v);
+void lsd_gemm_set_big_group(int v);
+void lsd_gemm_set_big_kind(int v);
 void lsd_gemm_set_tiled3_max(int v);
 void lsd_gemm_set_ring_slots(int v);
 void lsd_gemm_set_ring_tn(int v);
@@ -518,6 +520,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_stamps", &set_stamps);
   // tiled GEMMs with >= this many 256x256 tiles use the pipelined 256^2 kernel
   m.def("gemm_set_big_min", [](int64_t v) { lsd_gemm_set_big_min((int)v); });
+  // large-GEMM tile order: groups of this many row panels (0 = M-fastest)
+  m.def("gemm_set_big_group", [](int64_t v) { lsd_gemm_set_big_group((int)v); });
+  // large-GEMM kernel: 0 = BK=32 ring (gemm_big), 1 = phase-pipelined BK=64 (gemm_p8)
+  m.def("gemm_set_big_kind", [](int64_t v) { lsd_gemm_set_big_kind((int)v); });
   m.def("gemm_set_tiled3_max", [](int64_t v) { lsd_gemm_set_tiled3_max((int)v); });
   m.def("gemm_set_ring_slots", [](int64_t v) { lsd_gemm_set_ring_slots((int)v); });
   m.def("gemm_set_ring_tn", [](int64_t v) { lsd_gemm_set_ring_tn((int)v); });

@@ -781,15 +781,34 @@ __device__ __forceinline__ bf16x8 lds_frag_big(const char* op, int row, int g) {
   return *reinterpret_cast<const bf16x8*>(op + row * 64 + ((g ^ big_swz((row >> 2) & 3)) << 4));
 }
 
+// Tile order of the large GEMMs.  G = 0: M-fastest (consecutive workgroups
+// share a W panel).  G > 0: groups of G row panels, M-fastest inside a group
+// and the group's column panels in turn -- the tiles in flight at once (the
+// XCD-contiguous ranges of xcd_remap) then cover a few row panels instead of
+// sweeping every row panel per column panel, so each A panel is read from
+// HBM about once instead of once per column tile.
+__device__ __forceinline__ void tile_order(int t, int tiles_m, int tiles_n, int G, int& tm, int& tn) {
+  if (G <= 0) {
+    tm = t % tiles_m;
+    tn = t / tiles_m;
+    return;
+  }
+  const int gsz = G * tiles_n, grp = t / gsz, idx = t % gsz;
+  const int gm = min(G, tiles_m - grp * G);
+  tm = grp * G + idx % gm;
+  tn = idx / gm;
+}
+
 template <int EPI>
-__global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m, int tiles_n) {
+__global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
   __shared__ __attribute__((aligned(16))) char smem[GSMEM];
   const int nwg = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int per_split = tiles_m * tiles_n;
   const int split = bid / per_split;
   const int t = bid % per_split;
-  const int tm = t % tiles_m, tn = t / tiles_m;
+  int tm, tn;
+  tile_order(t, tiles_m, tiles_n, G, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int KT = p.K / 64;  // split boundaries in 64-deep units: ns is even
   const int kb = 2 * (int)((long)KT * split / p.splits);
@@ -935,9 +954,214 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m
 }
 
 // ---------------------------------------------------------------------------
+// Large GEMM, phase-pipelined (prefill): 256x256 tile, BK = 64, 8 waves,
+// two LDS buffers of four 16 KiB half-tiles, one glds half-tile per phase
+// ---------------------------------------------------------------------------
+// A K-tile t (64 deep) is held as four half-tiles in buffer t & 1:
+//   A0 = A rows m0 + [0, 128), A1 = A rows m0 + [128, 256),
+//   B0 = W rows n0 + [0, 128), B1 = W rows n0 + [128, 256),
+// each [128 rows][64 k] with 128-B rows, 16-B chunks XOR-swizzled by
+// (row >> 1) & 7 (the 128x128 kernel's conflict-free fragment image).
+// Wave (wr, wc) owns four 64 x 32 output blocks, one per (A half, B half):
+// rows mh * 128 + wr * 64 + [0, 64), columns nh * 128 + wc * 32 + [0, 32).
+// Each K-tile is four phases, one output quadrant (A half mh, B half nh) of
+// 16 MFMAs each, in the order (0,0) (0,1) (1,1) (1,0):
+//   phase  reads (ds_read_b128)       stages (glds, 2 per thread)  waits
+//   q0     A0 frags (8) + B0 frags (4)  B1 of tile t+1
+//   q1     B1 frags (4)                 A1 of tile t+1               A1(t)
+//   q2     A1 frags (8)                 A0 of tile t+2
+//   q3     --  (B0 frags kept)          B0 of tile t+2               A0/B0/B1(t+1)
+// so every half-tile is restaged >= 2 phases after its last read (A0 read
+// q0 -> restaged q2, B0 q0 -> q3, B1 q1 -> q0 next, A1 q2 -> q1 next) and is
+// issued 5-6 phases before it is read; the counted vmcnt waits (q1: 4
+// later halves in flight, q3: 3) always sit one phase before the first read
+// of what they retire.  Phase body: reads, stage, wait, s_barrier,
+// lgkmcnt(0), 16 MFMAs, s_barrier.  The two wave rows run staggered by one
+// barrier (wr = 1 takes an extra barrier up front, wr = 0 one at the end), so
+// on every SIMD one wave issues its LDS reads and DMA while the other runs
+// MFMAs (guide §5 "The 256^2 8-phase template").  All LDS is one array;
+// the epilogue reuses it as the fp32 C tile.
+constexpr int P8_HALF = 128 * 64 * 2;  // 16 KiB
+constexpr int P8_BUF = 4 * P8_HALF;    // A0 A1 B0 B1
+constexpr int P8_SMEM = 2 * P8_BUF;    // 128 KiB (== 256 x 128 fp32 C half-tile)
+
+__device__ __forceinline__ void p8_stage(char* lds, const bf16* src, long ld, int row0, int row_max,
+                                         int k0) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int inst = w * 2 + q;  // 16 x 1 KiB = 128 rows of 128 B
+    const int row = inst * 8 + (lane >> 3);
+    const int lch = (lane & 7) ^ ((row >> 1) & 7);
+    const bf16* gp = src + (long)min(row0 + row, row_max) * ld + k0 + lch * 8;
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)gp, (lds_void*)(lds + inst * 1024), 16, 0, 0);
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
+  __shared__ __attribute__((aligned(16))) char smem[P8_SMEM];
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int per_split = tiles_m * tiles_n;
+  const int split = bid / per_split;
+  int tm, tn;
+  tile_order(bid % per_split, tiles_m, tiles_n, G, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int KT = p.K / 64;
+  const int kb = (int)((long)KT * split / p.splits);
+  const int T = (int)((long)KT * (split + 1) / p.splits) - kb;  // K-tiles of this split
+
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int r = lane & 15, g = lane >> 4;
+
+  f32x4 acc[8][4];  // [mh * 4 + i][nh * 2 + j]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // half h of K-tile t: 0 = A0, 1 = A1, 2 = B0, 3 = B1
+  auto stage = [&](int t, int h) {
+    char* dst = smem + (t & 1) * P8_BUF + h * P8_HALF;
+    const int k0 = (kb + t) * 64;
+    if (h < 2) p8_stage(dst, p.A, p.lda, m0 + h * 128, p.M - 1, k0);
+    else p8_stage(dst, p.W, p.ldw, n0 + (h - 2) * 128, p.N - 1, k0);
+  };
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  auto read_a = [&](int t, int mh) {
+    const char* src = smem + (t & 1) * P8_BUF + mh * P8_HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = lds_frag(src, wr * 64 + i * 16 + r, kk * 4 + g);
+  };
+  auto read_b = [&](int t, int nh, bf16x8 (&bf)[2][2]) {
+    const char* src = smem + (t & 1) * P8_BUF + (2 + nh) * P8_HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = lds_frag(src, wc * 32 + j * 16 + r, kk * 4 + g);
+  };
+  auto mma = [&](int mh, int nh, bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_waitcnt(LGKM0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh * 4 + i][nh * 2 + j] = mfma16(af[i][kk], bf[j][kk], acc[mh * 4 + i][nh * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  if (T > 0) {
+    // prologue: all of tile 0, then A0 / B0 of tile 1; tile 0 published
+    stage(0, 0);
+    stage(0, 2);
+    stage(0, 3);
+    stage(0, 1);
+    if (T > 1) {
+      stage(1, 0);
+      stage(1, 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+
+    for (int t = 0; t < T; ++t) {
+      const bool n1 = t + 1 < T, n2 = t + 2 < T;
+      // q0: (A0, B0)
+      read_a(t, 0);
+      read_b(t, 0, b0);
+      if (n1) stage(t + 1, 3);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0, 0, b0);
+      // q1: (A0, B1); retire A1(t): 4 later halves in flight when t + 1 exists
+      read_b(t, 1, b1);
+      if (n1) stage(t + 1, 1);
+      if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0, 1, b1);
+      // q2: (A1, B1)
+      read_a(t, 1);
+      if (n2) stage(t + 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1, 1, b1);
+      // q3: (A1, B0); retire A0 / B0 / B1 of t + 1 (A1(t+1), A0 / B0(t+2) stay in flight)
+      if (n2) stage(t + 2, 2);
+      if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (n1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1, 0, b0);
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  }
+
+  // Epilogue: two passes over 128-column halves (nh), the fp32 C half-tile
+  // [256][128] staged in LDS (16-float chunks XOR-swizzled by (row >> 2) & 3),
+  // then 16-byte row-contiguous epilogue8 stores.
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = mh * 128 + wr * 64 + i * 16 + 4 * g + q;
+            const int col = wc * 32 + j * 16 + r;
+            ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[mh * 4 + i][h * 2 + j][q];
+          }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 256 * 16; c += 512) {
+      const int row = c >> 4, ch = c & 15, m = m0 + row, n = n0 + h * 128 + ch * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const float* src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if constexpr (EPI == EPI_SILU_MUL) {
+        if ((ch & 3) >= 2) continue;  // up chunks are read by their gate chunk
+        const float* up = ct + row * 128 + (((ch + 2) * 8) ^ (((row >> 2) & 3) << 4));
+        const f32x4 ulo = *reinterpret_cast<const f32x4*>(up);
+        const f32x4 uhi = *reinterpret_cast<const f32x4*>(up + 4);
+        const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
+        st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
+      } else {
+        epilogue8<EPI>(p, m, n, v, split);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
 static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
+// lsd_gemm_set_big_group(): tile_order() group (0 = M-fastest).  4: XL prefill
+// GEMMs 10-25 % faster than M-fastest, 8 equal, 16+ slower
+// (profiles/r2_prefill_tile_order.log)
+static int g_big_group = 4;
+// lsd_gemm_set_big_kind(): 0 = BK=32 ring kernel (gemm_big), 1 = phase-pipelined BK=64 (gemm_p8)
+static int g_big_kind = 1;
 // 128x128 launches of at most this many workgroups use the 3-slot ring kernel
 // (1 block/CU); larger grids keep the 2-blocks/CU double-buffered one.
 // lsd_gemm_set_tiled3_max(): tuning / tests; 0 = off
@@ -1007,7 +1231,12 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
   // tiles; the 128x128 kernel (2 blocks/CU) for smaller M / N.
   const int bm = (p.M + GBM - 1) / GBM, bn = (p.N + GBN - 1) / GBN;
   if (p.M >= GBM && p.K % 64 == 0 && bm * bn * p.splits >= g_big_min_blocks) {
-    hipLaunchKernelGGL((gemm_big_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn);
+    if (g_big_kind == 1)
+      hipLaunchKernelGGL((gemm_p8_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+                         g_big_group);
+    else
+      hipLaunchKernelGGL((gemm_big_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+                         g_big_group);
     return hipGetLastError();
   }
   const int tm = (p.M + TBM - 1) / TBM;
@@ -1038,6 +1267,8 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
 using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
+extern "C" void lsd_gemm_set_big_group(int v) { g_big_group = v < 0 ? 0 : v; }
+extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = v == 1 ? 1 : 0; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = v == 64 ? 64 : 128; }

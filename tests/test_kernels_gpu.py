@@ -213,7 +213,7 @@ def BIG(C):
     C.gemm_set_big_min(160)
 
 
-@pytest.mark.parametrize("M", [256, 300, 777])
+@pytest.mark.parametrize("M", [256, 300, 777, 1300])
 @pytest.mark.parametrize("K", [64, 128, 384])
 def test_big_gemm_epilogues(BIG, CNT, M, K):
     """256x256 ring-pipelined kernel: every epilogue, M/N tails, K of 2, 4 and 12

@@ -413,6 +413,16 @@ def main():
         for s in (0, 4, 8):
             bench_norm(64, H, s)
             bench_norm(128, H, s)
+    if "pgroup" in which:  # prefill GEMM tile order: row-panel groups
+        for G in (0, 4, 8, 16, 32):
+            C.gemm_set_big_group(G)
+            bench_prefill_gemms(65536, 1600, 6400, 25, 64, label=f"_xl_G{G}")
+        C.gemm_set_big_group(0)
+    if "p8" in which:  # large-GEMM kernel: BK=32 ring (0) vs phase-pipelined BK=64 (1)
+        for kind in (0, 1):
+            C.gemm_set_big_kind(kind)
+            bench_prefill_gemms(65536, 1600, 6400, 25, 64, label=f"_xl_kind{kind}")
+        C.gemm_set_big_kind(1)
     if "sample" in which:
         for B in (1, 64, 256):
             for g in (True, False):
