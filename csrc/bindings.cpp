@@ -24,6 +24,7 @@ void lsd_gemm_set_big_kind(int v);
 void lsd_gemm_set_tiled3_max(int v);
 void lsd_gemm_set_ring_slots(int v);
 void lsd_gemm_set_ring_tn(int v);
+void lsd_gemm_set_ring_fill(int v);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
 int lsd_gemm_sk_rows(int M, int N, int S);
@@ -527,6 +528,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_tiled3_max", [](int64_t v) { lsd_gemm_set_tiled3_max((int)v); });
   m.def("gemm_set_ring_slots", [](int64_t v) { lsd_gemm_set_ring_slots((int)v); });
   m.def("gemm_set_ring_tn", [](int64_t v) { lsd_gemm_set_ring_tn((int)v); });
+  m.def("gemm_set_ring_fill", [](int64_t v) { lsd_gemm_set_ring_fill((int)v); });
   // decode attention: cap the grid (blocks loop over (sequence, head) items)
   m.def("attn_set_max_wg", [](int64_t v) { lsd_attn_set_max_wg((int)v); });
   // decode attention: waves per block when the batch has few (sequence, head) items

@@ -1167,7 +1167,8 @@ static int g_big_kind = 1;
 // lsd_gemm_set_tiled3_max(): tuning / tests; 0 = off
 static int g_tiled3_max_blocks = 0;
 static int g_ring_slots = 3;  // lsd_gemm_set_ring_slots(): 3 or 4
-static int g_ring_tn = 128;   // lsd_gemm_set_ring_tn(): ring tile columns, 128 or 64
+static int g_ring_tn = 128;   // lsd_gemm_set_ring_tn(): ring tile columns, 128, 64, 32 or 0 (auto 32/64)
+static int g_ring_fill = 128; // auto: 32-wide tiles below this many 64-wide workgroups
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
 // with N = H), M > g_sk_rows rows run as ceil(M / g_sk_rows) row blocks
@@ -1240,10 +1241,20 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
     return hipGetLastError();
   }
   const int tm = (p.M + TBM - 1) / TBM;
-  if (g_ring_tn == 64) {  // narrow ring tiles: twice the workgroups of the 128-column grid
-    const int tn = (p.N + 63) / 64;
-    if (tm * tn * p.splits <= g_tiled3_max_blocks) {
-      hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 64>), dim3(tm * tn * p.splits), dim3(256), 0, st, p, tm, tn);
+  if (g_ring_tn == 64 || g_ring_tn == 32 || g_ring_tn == 0) {
+    // narrow ring tiles: twice the workgroups of the 128-column grid; 32-wide
+    // (2 blocks/CU) when 64-wide tiles leave the chip under-filled (auto, 0)
+    const int tn64 = (p.N + 63) / 64;
+    const bool narrow = g_ring_tn == 32 || (g_ring_tn == 0 && tm * tn64 * p.splits < g_ring_fill);
+    if (narrow && (p.N % 32) == 0) {
+      const int tn = (p.N + 31) / 32;
+      if (tm * tn * p.splits <= 2 * g_tiled3_max_blocks) {
+        hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 32>), dim3(tm * tn * p.splits), dim3(256), 0, st, p, tm, tn);
+        return hipGetLastError();
+      }
+    }
+    if (tm * tn64 * p.splits <= g_tiled3_max_blocks) {
+      hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 64>), dim3(tm * tn64 * p.splits), dim3(256), 0, st, p, tm, tn64);
       return hipGetLastError();
     }
   }
@@ -1271,7 +1282,8 @@ extern "C" void lsd_gemm_set_big_group(int v) { g_big_group = v < 0 ? 0 : v; }
 extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = v == 1 ? 1 : 0; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
-extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = v == 64 ? 64 : 128; }
+extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }
+extern "C" void lsd_gemm_set_ring_fill(int v) { g_ring_fill = v; }
 extern "C" int lsd_gemm_sk_rblocks(int M, int N, int S) { return sk_rblocks(M, N, S); }
 extern "C" int lsd_gemm_sk_rows(int M, int N, int S) {  // rows per row block
   return sk_mt(M, sk_rblocks(M, N, S)) * 16;

@@ -142,7 +142,12 @@ class HipBackend(Backend):
     # ring tile columns, 128 or 64.  128x64 tiles double the workgroups of the
     # decode-sized grids: at 256 rows QKV 20.5 -> 15.6 us, MLP-up 23.5 -> 17.3
     # (split-K kernel 23.3 / 26.2, hipBLASLt 19.3 / 20.0); bench 42.9k -> 43.8k
-    RING_TN = int(os.environ.get("LSD_RING_TN", "64"))
+    RING_TN = int(os.environ.get("LSD_RING_TN", "0"))
+    # auto (RING_TN = 0): 128x32 ring tiles (2 blocks/CU) when the 128x64 grid
+    # has fewer workgroups than this -- 128 rows: QKV 15.9 -> 13.2 us, MLP-up
+    # 17.2 -> 14.2; at 256 rows the 64-wide tiles stay faster (15.6 vs 18.6)
+    # (profiles/r2_ring_tn32.log)
+    RING_FILL = int(os.environ.get("LSD_RING_FILL", "128"))
     # Decode GEMMs leave split-K for the tiled kernels (the 128x64 LDS ring at
     # these grid sizes) above TILED_ALL_M rows at any width, and above
     # TILED_MIN_M rows when at least TILED_MIN_N wide.  bench tok/s (1 MI355X,
@@ -164,6 +169,7 @@ class HipBackend(Backend):
         self.C.gemm_set_tiled3_max(self.TILED3_MAX)
         self.C.gemm_set_ring_slots(self.RING_SLOTS)
         self.C.gemm_set_ring_tn(self.RING_TN)
+        self.C.gemm_set_ring_fill(self.RING_FILL)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))
@@ -216,7 +222,7 @@ class HipBackend(Backend):
 
     def _resid_splits(self, M: int, N: int, K: int) -> int:
         if self._tiled(M, N):
-            if M <= self.SK_MAX_M and self.TILED3_MAX and self.RING_TN == 64:
+            if M <= self.SK_MAX_M and self.TILED3_MAX and self.RING_TN in (0, 32, 64):
                 # decode rows on the 128x64 ring: as many splits as keep the
                 # grid on the ring kernel
                 tiles = math.ceil(M / 128) * math.ceil(N / 64)

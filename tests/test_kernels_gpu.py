@@ -162,10 +162,10 @@ def test_gemm_large_prefill_shape(C, CNT):
     close(C.linear(a, w, None, 0, True, 1, CNT), ref.linear(a, w), 3e-2)
 
 
-@pytest.fixture(params=[(3, 128), (4, 128), (3, 64)])
+@pytest.fixture(params=[(3, 128), (4, 128), (3, 64), (3, 32), (3, 0)])
 def RING(C, request):
     """Route every tiled launch to the LDS ring variant: 3 or 4 slots of
-    128x128 tiles, or 3 slots of 128x64 tiles."""
+    128x128 tiles, or 3 slots of 128x64 / 128x32 tiles (0: auto width)."""
     slots, tn = request.param
     C.gemm_set_tiled3_max(1 << 30)
     C.gemm_set_ring_slots(slots)

@@ -272,6 +272,43 @@ def bench_sample(B, V, greedy):
     report(f"sample B={B} V={V} greedy={greedy}", us, B * V * 4)
 
 
+def bench_ring_tn(M, H=1600, F=6400):
+    """Decode-sized ring GEMMs: 128x64 vs 128x32 tiles (2 blocks/CU), rotating
+    weights; residual projections with their slab combine at several splits."""
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    C.gemm_set_tiled3_max(512)  # the engine's ring cap (HipBackend.TILED3_MAX)
+    a = torch.randn(M, H, device=DEV).bfloat16()
+    af = torch.randn(M, F, device=DEV).bfloat16()
+    x = torch.randn(M, H, device=DEV)
+    shapes = {"qkv": (3 * H, H), "fc": (F, H), "proj": (H, H), "proj2": (H, F)}
+    ws = {k: rotating(lambda n=n, k_=k_: torch.randn(n, k_, device=DEV).bfloat16(), n * k_ * 2)
+          for k, (n, k_) in shapes.items()}
+    for tn in (64, 32):
+        C.gemm_set_ring_tn(tn)
+        for name in ("qkv", "fc"):
+            it = [0]
+            N, K = shapes[name]
+
+            def run(name=name, it=it):
+                w = ws[name][it[0] % len(ws[name])]
+                it[0] += 1
+                C.linear(a, w, None, 1 if name == "fc" else 0, True, 1, cnt)
+            report(f"ring_tn{tn}_{name} M={M} N={N} K={K}", timeit(run), N * K * 2)
+        for name in ("proj", "proj2"):
+            N, K = shapes[name]
+            inp = a if name == "proj" else af
+            for S in (2, 3, 5, 8):
+                it = [0]
+
+                def run(name=name, it=it, S=S, inp=inp):
+                    w = ws[name][it[0] % len(ws[name])]
+                    it[0] += 1
+                    slab = C.linear_residual(inp, w, None, x, S, True, cnt, True)
+                    C.norm(x, slab, None, None, None, 0.0, True, None, False)
+                report(f"ring_tn{tn}_{name}+combine M={M} N={N} K={K} S={S}", timeit(run), N * K * 2)
+    C.gemm_set_ring_tn(64)
+
+
 def stamps_gemm(M, N, K, splits, act=0, label=""):
     """Per-workgroup phase timeline of one decode-GEMM launch (diagnostic)."""
     w = torch.randn(N, K, device=DEV).bfloat16()
@@ -423,6 +460,9 @@ def main():
             C.gemm_set_big_kind(kind)
             bench_prefill_gemms(65536, 1600, 6400, 25, 64, label=f"_xl_kind{kind}")
         C.gemm_set_big_kind(1)
+    if "tn32" in which:
+        for M in (128, 256):
+            bench_ring_tn(M)
     if "sample" in which:
         for B in (1, 64, 256):
             for g in (True, False):
