@@ -309,6 +309,80 @@ def bench_ring_tn(M, H=1600, F=6400):
     C.gemm_set_ring_tn(64)
 
 
+def bench_corun(B=256, H=1600, F=6400, nh=25, hd=64, ctx=192, L=12):
+    """Co-running on two streams: an attention chain (HBM-bound) beside a
+    decode-GEMM chain (latency-bound), each captured as a graph; wall time
+    alone vs together (the overlap a de-phased second microbatch lane can get)."""
+    cnt = torch.zeros(2, 1 << 16, dtype=torch.int32, device=DEV)
+    C.gemm_set_tiled3_max(512)
+    C.gemm_set_ring_tn(0)
+    kcs = [torch.randn(B, nh, ctx + 1, hd, device=DEV).bfloat16() for _ in range(L)]
+    vcs = [torch.randn(B, nh, ctx + 1, hd, device=DEV).bfloat16() for _ in range(L)]
+    q = torch.randn(B, nh * hd, device=DEV).bfloat16()
+    ss = torch.arange(B, dtype=torch.int32, device=DEV)
+    pos = torch.full((B,), ctx - 1, dtype=torch.int32, device=DEV)
+    a = torch.randn(B, H, device=DEV).bfloat16()
+    af = torch.randn(B, F, device=DEV).bfloat16()
+    x = torch.randn(B, H, device=DEV)
+    wq = [torch.randn(3 * H, H, device=DEV).bfloat16() for _ in range(L)]
+    wf = [torch.randn(F, H, device=DEV).bfloat16() for _ in range(L)]
+    wp = [torch.randn(H, H, device=DEV).bfloat16() for _ in range(L)]
+    wp2 = [torch.randn(H, F, device=DEV).bfloat16() for _ in range(L)]
+
+    def attn_chain():
+        for i in range(L):
+            C.attn_decode(q, kcs[i], vcs[i], ss, pos, nh, 1)
+
+    def gemm_chain():
+        for i in range(L):
+            C.linear(a, wq[i], None, 0, True, 1, cnt[1])
+            s = C.linear_residual(a, wp[i], None, x, 5, True, cnt[1], True)
+            C.norm(x, s, None, None, None, 0.0, True, None, False)
+            C.linear(a, wf[i], None, 1, True, 1, cnt[1])
+            s = C.linear_residual(af, wp2[i], None, x, 5, True, cnt[1], True)
+            C.norm(x, s, None, None, None, 0.0, True, None, False)
+
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    graphs = []
+    for fn, st in ((attn_chain, sa), (gemm_chain, sb)):
+        with torch.cuda.stream(st):
+            fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            fn()
+        graphs.append(g)
+    ga, gb = graphs
+
+    def wall(run_a, run_b, reps=5):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            cur = torch.cuda.current_stream()
+            s.record(cur)
+            sa.wait_stream(cur)
+            sb.wait_stream(cur)
+            if run_a:
+                with torch.cuda.stream(sa):
+                    ga.replay()
+            if run_b:
+                with torch.cuda.stream(sb):
+                    gb.replay()
+            cur.wait_stream(sa)
+            cur.wait_stream(sb)
+            e.record(cur)
+            torch.cuda.synchronize()
+            ts.append(s.elapsed_time(e) * 1e3 / L)
+        return sorted(ts)[len(ts) // 2]
+
+    ta, tb, tab = wall(True, False), wall(False, True), wall(True, True)
+    report(f"corun B={B} ctx={ctx} per layer: attn alone", ta, 0)
+    report(f"corun B={B} ctx={ctx} per layer: gemms+norms alone", tb, 0)
+    report(f"corun B={B} ctx={ctx} per layer: both on two streams", tab, 0,
+           {"sum_us": round(ta + tb, 2), "overlap_saved_us": round(ta + tb - tab, 2)})
+
+
 def stamps_gemm(M, N, K, splits, act=0, label=""):
     """Per-workgroup phase timeline of one decode-GEMM launch (diagnostic)."""
     w = torch.randn(N, K, device=DEV).bfloat16()
@@ -463,6 +537,8 @@ def main():
     if "tn32" in which:
         for M in (128, 256):
             bench_ring_tn(M)
+    if "corun" in which:
+        bench_corun()
     if "sample" in which:
         for B in (1, 64, 256):
             for g in (True, False):
