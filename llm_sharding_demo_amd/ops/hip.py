@@ -225,9 +225,13 @@ class HipBackend(Backend):
             if M <= self.SK_MAX_M and self.TILED3_MAX and self.RING_TN in (0, 32, 64):
                 # decode rows on the 128x64 ring: as many splits as keep the
                 # grid on the ring kernel
+                # at most one split per 512 of K: short-K projections lose more
+                # to the slab combine than they gain in workgroups (GPT-2 XL
+                # attention out-proj, K = 1600: 3 splits 11.8 us vs 5 splits
+                # 12.6 at 256 rows, 9.2 vs 9.3 at 128; profiles/r2_ring_tn32.log)
                 tiles = math.ceil(M / 128) * math.ceil(N / 64)
                 target = min(self.TILED3_MAX, self.RING_RESID_TARGET or self.TILED3_MAX)
-                return max(1, min(target // tiles, K // 64 // 2 or 1))
+                return max(1, min(target // tiles, K // 512 or 1))
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
             return max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
         if self.DEFER_RESID:
