@@ -1008,6 +1008,7 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
   int tm, tn;
   tile_order(bid % per_split, tiles_m, tiles_n, G, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
+  LSD_STAMP(0)
   const int KT = p.K / 64;
   const int kb = (int)((long)KT * split / p.splits);
   const int T = (int)((long)KT * (split + 1) / p.splits) - kb;  // K-tiles of this split
@@ -1044,8 +1045,17 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) bf[j][kk] = lds_frag(src, wc * 32 + j * 16 + r, kk * 4 + g);
   };
+#ifdef LSD_P8_PROF
+  // diagnostic build only (LSD_HIPCC_FLAGS=-DLSD_P8_PROF): wave 0's cycles in
+  // the loop, in the counted vmcnt waits and in the two barriers of a phase
+  long long pf_t0 = 0, pf_vm = 0, pf_b1 = 0, pf_b2 = 0, pf_c = 0;
+#define P8_T() __builtin_amdgcn_s_memtime()
+#define P8_ACC(acc, stmt) { pf_c = P8_T(); stmt; acc += P8_T() - pf_c; }
+#else
+#define P8_ACC(acc, stmt) stmt;
+#endif
   auto mma = [&](int mh, int nh, bf16x8 (&bf)[2][2]) {
-    __builtin_amdgcn_s_barrier();
+    P8_ACC(pf_b1, __builtin_amdgcn_s_barrier())
     __builtin_amdgcn_s_waitcnt(LGKM0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -1058,7 +1068,7 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
           acc[mh * 4 + i][nh * 2 + j] = mfma16(af[i][kk], bf[j][kk], acc[mh * 4 + i][nh * 2 + j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    P8_ACC(pf_b2, __builtin_amdgcn_s_barrier())
   };
 
   if (T > 0) {
@@ -1075,8 +1085,12 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
+    LSD_STAMP(1)
     if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
 
+#ifdef LSD_P8_PROF
+    pf_t0 = P8_T();
+#endif
     for (int t = 0; t < T; ++t) {
       const bool n1 = t + 1 < T, n2 = t + 2 < T;
       // q0: (A0, B0)
@@ -1088,8 +1102,8 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
       // q1: (A0, B1); retire A1(t): 4 later halves in flight when t + 1 exists
       read_b(t, 1, b1);
       if (n1) stage(t + 1, 1);
-      if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      P8_ACC(pf_vm, if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory"))
       __builtin_amdgcn_sched_barrier(0);
       mma(0, 1, b1);
       // q2: (A1, B1)
@@ -1099,13 +1113,24 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
       mma(1, 1, b1);
       // q3: (A1, B0); retire A0 / B0 / B1 of t + 1 (A1(t+1), A0 / B0(t+2) stay in flight)
       if (n2) stage(t + 2, 2);
-      if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if (n1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      P8_ACC(pf_vm, if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                    else if (n1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"))
       __builtin_amdgcn_sched_barrier(0);
       mma(1, 0, b0);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+#ifdef LSD_P8_PROF
+    if (p.stamps && threadIdx.x == 0) {
+      long long* ps = p.stamps + (long)blockIdx.x * 8;
+      ps[4] = P8_T() - pf_t0;
+      ps[5] = pf_vm;
+      ps[6] = pf_b1;
+      ps[7] = pf_b2;
+    }
+#endif
   }
+#undef P8_ACC
+  LSD_STAMP(2)
 
   // Epilogue: two passes over 128-column halves (nh), the fp32 C half-tile
   // [256][128] staged in LDS (16-float chunks XOR-swizzled by (row >> 2) & 3),
@@ -1150,6 +1175,7 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
       }
     }
   }
+  LSD_STAMP(3)
 }
 
 // ---------------------------------------------------------------------------

@@ -383,6 +383,39 @@ def bench_corun(B=256, H=1600, F=6400, nh=25, hd=64, ctx=192, L=12):
            {"sum_us": round(ta + tb, 2), "overlap_saved_us": round(ta + tb - tab, 2)})
 
 
+def stamps_p8(M=65536, N=6400, K=1600, act=1):
+    """Per-workgroup phase timeline of the phase-pipelined prefill GEMM:
+    prologue (first K-tiles landed), main loop, epilogue; 100 MHz stamps."""
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16()
+    nb = ((M + 255) // 256) * ((N + 255) // 256)
+    st = torch.zeros(nb * 8, dtype=torch.int64, device=DEV)
+    C.gemm_set_big_min(1)
+    for _ in range(2):
+        C.linear(a, w, b, act, True, 1, None)
+    torch.cuda.synchronize()
+    C.set_stamps(st)
+    C.linear(a, w, b, act, True, 1, None)
+    torch.cuda.synchronize()
+    C.set_stamps(None)
+    C.gemm_set_big_min(160)
+    t = st.view(nb, 8).cpu().double()
+    us = lambda x: x * 10 / 1000  # noqa: E731
+    q = lambda x: [round(float(x.quantile(v)), 2) for v in (0.0, 0.1, 0.5, 0.9, 1.0)]  # noqa: E731
+    row = {"case": f"stamps_p8 M={M} N={N} K={K} blocks={nb}",
+           "prologue_us": q(us(t[:, 1] - t[:, 0])), "main_us": q(us(t[:, 2] - t[:, 1])),
+           "epilogue_us": q(us(t[:, 3] - t[:, 2])), "block_us": q(us(t[:, 3] - t[:, 0])),
+           "span_us": round(float(us(t[:, 3].max() - t[:, 0].min())), 1),
+           "sum_block_us_per_cu": round(float(us(t[:, 3] - t[:, 0]).sum()) / 256, 1)}
+    if t[:, 4].abs().sum() > 0:  # LSD_P8_PROF build: wave 0's loop cycles and where they went
+        lp = t[:, 4]
+        row.update({"loop_kcyc": q(lp / 1e3), "vmcnt_wait_frac": q(t[:, 5] / lp),
+                    "barrier1_frac": q(t[:, 6] / lp), "barrier2_frac": q(t[:, 7] / lp)})
+    RESULTS.append(row)
+    print(json.dumps(row), flush=True)
+
+
 def stamps_gemm(M, N, K, splits, act=0, label=""):
     """Per-workgroup phase timeline of one decode-GEMM launch (diagnostic)."""
     w = torch.randn(N, K, device=DEV).bfloat16()
@@ -539,6 +572,9 @@ def main():
             bench_ring_tn(M)
     if "corun" in which:
         bench_corun()
+    if "p8stamps" in which:
+        stamps_p8()
+        stamps_p8(N=1600, K=6400, act=0)
     if "sample" in which:
         for B in (1, 64, 256):
             for g in (True, False):
