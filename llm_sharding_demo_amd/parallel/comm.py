@@ -206,11 +206,16 @@ class NcclTransport(_DistTransport):
 
     def send(self, t, dst, edge):
         g = self._edge_group(edge, self.rank, dst)
+        if not t.is_contiguous():  # p2p needs a dense buffer (views of padded rows)
+            t = t.contiguous()
         return SendHandle(self.dist.isend(t, self._g(dst), group=g))
 
     def irecv(self, out, src, edge):
         g = self._edge_group(edge, src, self.rank)
-        return Handle(out, self.dist.irecv(out, self._g(src), group=g))
+        if out.is_contiguous():
+            return Handle(out, self.dist.irecv(out, self._g(src), group=g))
+        tmp = torch.empty(out.shape, dtype=out.dtype, device=out.device)
+        return Handle(out, self.dist.irecv(tmp, self._g(src), group=g), post=lambda: out.copy_(tmp))
 
 
 class GlooTransport(_DistTransport):
