@@ -14,10 +14,15 @@
 //                        batching scheduler drains it at every decode step
 //                        (try_pop); window/length-group round formation
 //                        (next_groups) for batch jobs.
+//   * SchedCore       -- the continuous-batching state machine (sched_core.h):
+//                        admission into slots, per-step group plans (leaves,
+//                        joins, prefill chunks, decode rows / buckets), token
+//                        readout events and slot release.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include "batch_queue.h"
+#include "sched_core.h"
 
 #include <algorithm>
 #include <cmath>
@@ -29,40 +34,7 @@
 
 namespace py = pybind11;
 
-class SlotAllocator {
- public:
-  explicit SlotAllocator(int n) : cap_(n), used_(n, false) {
-    for (int i = n - 1; i >= 0; --i) free_.push_back(i);
-  }
-  std::vector<int> alloc(int k) {
-    if (k > (int)free_.size())
-      throw std::runtime_error("out of KV slots: want " + std::to_string(k) + ", have " +
-                               std::to_string(free_.size()));
-    std::vector<int> out;
-    out.reserve(k);
-    for (int i = 0; i < k; ++i) {
-      int s = free_.back();
-      free_.pop_back();
-      used_[s] = true;
-      out.push_back(s);
-    }
-    return out;
-  }
-  void free(const std::vector<int>& slots) {
-    for (int s : slots) {
-      if (s < 0 || s >= cap_ || !used_[s]) throw std::runtime_error("double free / bad slot " + std::to_string(s));
-      used_[s] = false;
-      free_.push_back(s);
-    }
-  }
-  int available() const { return (int)free_.size(); }
-  int capacity() const { return cap_; }
-
- private:
-  int cap_;
-  std::vector<bool> used_;
-  std::vector<int> free_;
-};
+using lsd_rt::SlotAllocator;
 
 // costs[i] = cost of layer i; head = extra cost of the last stage.
 std::vector<std::pair<int, int>> partition_minmax(const std::vector<double>& costs, int P,
@@ -119,4 +91,28 @@ PYBIND11_MODULE(_runtime, m) {
       .def_property_readonly("max_seen", &BatchQueue::max_seen)
       .def_property_readonly("pushed", &BatchQueue::pushed)
       .def_property_readonly("popped", &BatchQueue::popped);
+  using lsd_rt::SchedCore;
+  py::class_<SchedCore>(m, "SchedCore")
+      .def(py::init<int, int, int, int64_t, int, int, std::vector<SlotAllocator*>>(),
+           py::arg("replicas"), py::arg("groups"), py::arg("cap"), py::arg("prefill_budget"),
+           py::arg("chunk"), py::arg("max_seq"), py::arg("pools"),
+           py::keep_alive<1, 8>())  // the pools outlive the core
+      .def("add", &SchedCore::add, py::arg("sid"), py::arg("prompt_len"), py::arg("want"),
+           py::arg("stop_at_eos"))
+      .def("has_work", &SchedCore::has_work)
+      .def("plan", [](SchedCore& c, int64_t step) {
+             std::vector<int64_t> admitted;
+             auto p = c.plan(step, &admitted);
+             return py::make_tuple(p, admitted);
+           }, py::arg("step"))
+      .def("assign", &SchedCore::assign, py::arg("rep"), py::arg("step"), py::arg("g"),
+           py::arg("tokens"), py::arg("eos"))
+      .def("reset", &SchedCore::reset)
+      .def_property_readonly("joins", &SchedCore::joins)
+      .def_property_readonly("leaves", &SchedCore::leaves)
+      .def_property_readonly("max_rows", &SchedCore::max_rows)
+      .def_property_readonly("steps", &SchedCore::steps)
+      .def_property_readonly("n_waiting", &SchedCore::n_waiting)
+      .def_property_readonly("n_seqs", &SchedCore::n_seqs)
+      .def_property_readonly("n_expect", &SchedCore::n_expect);
 }

@@ -16,6 +16,7 @@ PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(ROOT, "csrc", "runtime", "runtime.cpp")
 HDR = os.path.join(ROOT, "csrc", "runtime", "batch_queue.h")
+CORE = os.path.join(ROOT, "csrc", "runtime", "sched_core.h")
 
 
 def build(force: bool = False) -> str:
@@ -27,7 +28,7 @@ def build(force: bool = False) -> str:
     flags = ["-O2", "-std=c++17", "-fPIC", "-shared", f"-I{pybind11.get_include()}",
              f"-I{sysconfig.get_paths()['include']}"]
     h = hashlib.sha1(" ".join(flags).encode())
-    for src in (SRC, HDR):
+    for src in (SRC, HDR, CORE):
         with open(src, "rb") as f:
             h.update(f.read())
     sig = h.hexdigest()

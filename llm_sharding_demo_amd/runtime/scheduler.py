@@ -176,16 +176,19 @@ def make_batch_queue(max_batch: int, length_ratio: float = 4.0, native: bool = T
 
 
 # ---------------------------------------------------------------------------
-# Scheduler
+# Scheduler core: the per-step state machine (native csrc/runtime/sched_core.h,
+# or this Python twin -- same interface, same plans, compared in
+# tests/test_sched_core.py)
 # ---------------------------------------------------------------------------
 
+EV_FIRST, EV_FINISH, EV_RELEASE = 1, 2, 4
+
+
 @dataclass
-class Seq:
-    id: int
-    req: Request
-    prompt: List[int]
-    params: SamplingParams
-    seed: int
+class _Seq:
+    prompt_len: int
+    want: int
+    stop_at_eos: bool
     rep: int = 0
     g: int = -1
     slot: int = -1
@@ -193,31 +196,26 @@ class Seq:
     issued: int = 0             # output tokens whose production has been issued
     pos: int = 0                # next decode input position
     sstep: int = 1              # sampler counter of the next decode draw
-    tokens: List[int] = field(default_factory=list)
+    ntok: int = 0               # tokens read back
     stop: bool = False          # EOS read back (stop_at_eos): leave at the next step
-    left: bool = False
-
-    @property
-    def want(self) -> int:
-        return self.params.max_new_tokens
+    finished: bool = False
 
 
 @dataclass
-class Produced:
+class _Produced:
     """Composition of one item that produced tokens: how to read its
     token-return vector [decode rows (b) | final prefill chunks]."""
     b: int
     rows: List[int]             # seq ids of decode rows [0, n)
     finals: List[int]           # seq ids whose final prefill chunk was sampled
     release: List[int] = field(default_factory=list)  # seqs whose last item this was
-    step: int = 0
 
 
 @dataclass
-class GroupHost:
+class _Group:
     rows: List[int] = field(default_factory=list)
     prefilling: List[int] = field(default_factory=list)
-    prev: Optional[Produced] = None
+    prev: Optional[_Produced] = None
 
 
 def _bucket(n: int, cap: int) -> int:
@@ -229,11 +227,208 @@ def _bucket(n: int, cap: int) -> int:
     return min(b, cap)
 
 
+class PySchedCore:
+    """Python twin of lsd_rt::SchedCore (LSD_PY_RUNTIME=1, or no native
+    runtime).  plan(step) -> ([per replica: [(g, ret, n, b, ctxb, rows_changed,
+    chunks [(sid, slot, start, len, final)], rows [(sid, slot, pos, sstep,
+    src)])]], admitted sids); assign(...) -> [(sid, token, flags)]."""
+
+    def __init__(self, replicas: int, groups: int, cap: int, prefill_budget: int, chunk: int,
+                 max_seq: int, pools):
+        self.R, self.M, self.cap = replicas, groups, cap
+        self.budget, self.chunk, self.max_seq = prefill_budget, chunk, max_seq
+        self.pools = list(pools)
+        self.seqs: Dict[int, _Seq] = {}
+        self.waiting: Deque[int] = collections.deque()
+        self.groups = [[_Group() for _ in range(groups)] for _ in range(replicas)]
+        self.expect: Dict[tuple, _Produced] = {}
+        self.joins = self.leaves = self.max_rows = self.steps = 0
+
+    def add(self, sid: int, prompt_len: int, want: int, stop_at_eos: bool) -> None:
+        if prompt_len <= 0:
+            raise ValueError("empty prompt")
+        self.seqs[sid] = _Seq(prompt_len, want, stop_at_eos)
+        self.waiting.append(sid)
+
+    def has_work(self) -> bool:
+        if self.waiting:
+            return True
+        return any(g.rows or g.prefilling or g.prev is not None for rep in self.groups for g in rep)
+
+    @property
+    def n_waiting(self) -> int:
+        return len(self.waiting)
+
+    @property
+    def n_seqs(self) -> int:
+        return len(self.seqs)
+
+    @property
+    def n_expect(self) -> int:
+        return len(self.expect)
+
+    def plan(self, step: int):
+        admitted: List[int] = []
+        out = []
+        for rep in range(self.R):
+            gs = []
+            for g in range(self.M):
+                go = self._group_plan(rep, g, step, admitted)
+                if go is not None:
+                    gs.append(go)
+            out.append(gs)
+        self.steps += 1
+        return out, admitted
+
+    def _admit(self, rep: int, g: int, room: int, admitted: List[int]) -> List[int]:
+        pool = self.pools[rep]
+        out = []
+        while self.waiting and room > 0 and pool.available > 0:
+            sid = self.waiting.popleft()
+            s = self.seqs[sid]
+            s.rep, s.g = rep, g
+            s.slot = pool.alloc(1)[0]
+            out.append(sid)
+            admitted.append(sid)
+            room -= 1
+            self.joins += 1
+        return out
+
+    def _group_plan(self, rep: int, g: int, step: int, admitted: List[int]):
+        gh = self.groups[rep][g]
+        prev, gh.prev = gh.prev, None
+        ret = prev.b + len(prev.finals) if prev is not None else 0
+        # leaves: every token scheduled, or EOS read back
+        keep = []
+        for sid in gh.rows:
+            s = self.seqs[sid]
+            if s.issued >= s.want or s.stop:
+                self.leaves += 1
+                if prev is not None:
+                    prev.release.append(sid)
+            else:
+                keep.append(sid)
+        new_rows = keep + (list(prev.finals) if prev is not None else [])
+        changed = new_rows != gh.rows
+        # joins (capacity counts rows + sequences still prefilling)
+        room = self.cap - len(new_rows) - len(gh.prefilling)
+        gh.prefilling += self._admit(rep, g, room, admitted)
+        # prefill chunks (FIFO, one chunk per sequence per step, token budget)
+        budget = self.budget or (1 << 62)
+        chunks, finals = [], []
+        for sid in list(gh.prefilling):
+            s = self.seqs[sid]
+            L = s.prompt_len
+            n = L - s.prefilled if self.chunk <= 0 else min(self.chunk, L - s.prefilled)
+            if chunks and n > budget:
+                break
+            budget -= n
+            a = s.prefilled
+            final = a + n == L
+            chunks.append((sid, s.slot, a, n, final))
+            s.prefilled += n
+            if final:
+                gh.prefilling.remove(sid)
+                finals.append(sid)
+                s.issued, s.pos, s.sstep = 1, L, 1
+        # decode rows
+        n = len(new_rows)
+        b = _bucket(n, self.cap)
+        rows = []
+        if changed:
+            old_index = {sid: i for i, sid in enumerate(gh.rows)}
+            for sid in new_rows:
+                s = self.seqs[sid]
+                src = old_index[sid] if sid in old_index else prev.b + prev.finals.index(sid)
+                rows.append((sid, s.slot, s.pos, s.sstep, src))
+        ctxb = 0
+        if n:
+            top = max(self.seqs[sid].pos for sid in new_rows) + 1
+            ctxb = min(-(-top // 256) * 256, self.max_seq)
+            for sid in new_rows:  # this step issues one token per decode row
+                s = self.seqs[sid]
+                s.issued += 1
+                s.pos += 1
+                s.sstep += 1
+        gh.rows = new_rows
+        self.max_rows = max(self.max_rows, n)
+        if b or finals:
+            gh.prev = _Produced(b, list(new_rows), finals)
+        if prev is not None:  # its readout comes back in this step's token-return vector
+            self.expect[(rep, step, g)] = prev
+        if not (ret or b or chunks):
+            return None
+        return (g, ret, n, b, ctxb, changed, chunks, rows)
+
+    def assign(self, rep: int, step: int, g: int, tokens: List[int], eos: int):
+        prod = self.expect.pop((rep, step, g))
+        ev = []
+        for i, sid in enumerate(prod.rows):
+            self._give(sid, tokens[i], eos, ev)
+        for j, sid in enumerate(prod.finals):
+            self._give(sid, tokens[prod.b + j], eos, ev)
+        for sid in prod.release:
+            s = self.seqs.pop(sid, None)
+            if s is None:
+                continue
+            if s.slot >= 0:
+                self.pools[s.rep].free([s.slot])
+            ev.append((sid, -1, EV_RELEASE | (0 if s.finished else EV_FINISH)))
+        return ev
+
+    def _give(self, sid: int, tok: int, eos: int, ev: list) -> None:
+        s = self.seqs.get(sid)
+        if s is None or s.finished or s.ntok >= s.want:
+            return
+        flags = EV_FIRST if s.ntok == 0 else 0
+        s.ntok += 1
+        if s.stop_at_eos and tok == eos:
+            s.stop = True
+        if s.ntok >= s.want or s.stop:
+            s.finished = True
+            flags |= EV_FINISH
+        ev.append((sid, tok, flags))
+
+    def reset(self) -> None:
+        for s in self.seqs.values():
+            if s.slot >= 0:
+                self.pools[s.rep].free([s.slot])
+        self.seqs.clear()
+        self.waiting.clear()
+        self.expect.clear()
+        self.groups = [[_Group() for _ in range(self.M)] for _ in range(self.R)]
+
+
+def make_sched_core(replicas: int, groups: int, cap: int, prefill_budget: int, chunk: int,
+                    max_seq: int, pools):
+    """The native core when the runtime is built and the slot pools are its
+    allocators; the Python twin otherwise (LSD_PY_RUNTIME=1)."""
+    from .native import load
+
+    rt = load()
+    if rt is not None and hasattr(rt, "SchedCore") and all(isinstance(p, rt.SlotAllocator) for p in pools):
+        return rt.SchedCore(replicas, groups, cap, prefill_budget, chunk, max_seq, list(pools))
+    return PySchedCore(replicas, groups, cap, prefill_budget, chunk, max_seq, pools)
+
+
+# ---------------------------------------------------------------------------
+# Scheduler
+# ---------------------------------------------------------------------------
+
+@dataclass
+class _Meta:
+    req: Request
+    seed: int
+    tokens: List[int] = field(default_factory=list)
+
+
 class Scheduler:
     """Continuous-batching scheduler for one engine (every pipeline replica).
 
-    Runs on the thread that drives stage 0 of replica 0.  `run_until()` is
-    the loop; `submit()` is thread-safe."""
+    Runs on the thread that drives stage 0 of replica 0 (`Engine._drive`);
+    `submit()` is thread-safe.  The per-step state machine lives in the
+    scheduler core (`make_sched_core`); this class owns the request futures,
+    the sampling parameters, the plan objects and the GPU readouts."""
 
     def __init__(self, engine, groups: int, cap: int):
         self.eng = engine
@@ -243,19 +438,16 @@ class Scheduler:
         self._pending: Dict[int, Request] = {}
         self._ids = itertools.count()
         self._plock = threading.Lock()
-        self.seqs: Dict[int, Seq] = {}
-        self.waiting: Deque[int] = collections.deque()     # admitted to the scheduler, not yet joined
-        self.groups = [[GroupHost() for _ in range(groups)] for _ in range(self.R)]
+        self.meta: Dict[int, _Meta] = {}
+        self.core = make_sched_core(self.R, groups, cap, engine.cfg.prefill_budget,
+                                    engine.cfg.prefill_chunk, engine.max_seq, engine.slot_pools)
         self.step = 0
-        self.readouts: Deque[tuple] = collections.deque()  # (step, ready(), tokens(), Produced)
+        self.readouts: Deque[tuple] = collections.deque()  # (step, ready(), sync(), tokens, key)
         self.lock = threading.RLock()                       # one driver at a time
         self.timing = False
         self.step_log: List[tuple] = []                     # (step, had_prefill) of timed steps
         self.stats = {"steps": 0, "joins": 0, "leaves": 0, "max_rows": 0, "captures": 0}
-        self.prefill_budget = engine.cfg.prefill_budget
-        self.chunk = engine.cfg.prefill_chunk
         self._rng = engine._rng
-        self._expect: Dict[tuple, Produced] = {}   # (replica, step, group) -> item awaiting readout
 
     # -- admission ---------------------------------------------------------
     def submit(self, prompt_ids: List[int], params: SamplingParams) -> Request:
@@ -274,218 +466,122 @@ class Scheduler:
 
     @property
     def queue_depth(self) -> int:
-        return self.queue.depth + len(self.waiting)
+        return self.queue.depth + self.core.n_waiting
 
     def _take_new(self) -> None:
         ids = self.queue.try_pop(1 << 20)
         with self._plock:
             reqs = [(i, self._pending.pop(i)) for i in ids]
         for i, req in reqs:
-            seed = req.params.seed if req.params.seed is not None else self._rng.getrandbits(62)
-            self.seqs[i] = Seq(i, req, req.prompt_ids, req.params, seed)
-            self.waiting.append(i)
+            p = req.params
+            seed = p.seed if p.seed is not None else self._rng.getrandbits(62)
+            self.meta[i] = _Meta(req, seed)
+            self.core.add(i, len(req.prompt_ids), p.max_new_tokens, bool(p.stop_at_eos))
 
     def has_work(self) -> bool:
-        if self.waiting or self.queue.depth:
-            return True
-        for rep in self.groups:
-            for gh in rep:
-                if gh.rows or gh.prefilling or gh.prev is not None:
-                    return True
-        return False
+        return bool(self.queue.depth) or self.core.has_work()
 
     # -- plan building ---------------------------------------------------------
-    def _admit(self, rep: int, gh_idx: int, room: int) -> List[int]:
-        pool = self.eng.slot_pools[rep]
-        out = []
-        while self.waiting and room > 0 and pool.available > 0:
-            sid = self.waiting.popleft()
-            s = self.seqs[sid]
-            s.rep, s.g = rep, gh_idx
-            s.slot = pool.alloc(1)[0]
-            s.req.t_start = time.monotonic()
-            out.append(sid)
-            room -= 1
-            self.stats["joins"] += 1
-        return out
-
-    def _group_plan(self, rep: int, g: int, step: int) -> Optional[GroupPlan]:
-        gh = self.groups[rep][g]
-        gp = GroupPlan(g)
-        prev = gh.prev
-        gh.prev = None
-        if prev is not None:
-            gp.ret = prev.b + len(prev.finals)
-        # leaves: every token scheduled, or EOS read back
-        keep = []
-        for sid in gh.rows:
-            s = self.seqs[sid]
-            if s.issued >= s.want or s.stop:
-                s.left = True
-                self.stats["leaves"] += 1
-                if prev is not None:
-                    prev.release.append(sid)
-            else:
-                keep.append(sid)
-        act = list(prev.finals) if prev is not None else []
-        new_rows = keep + act
-        changed = new_rows != gh.rows
-        # joins (capacity counts rows + sequences still prefilling)
-        room = self.cap - len(new_rows) - len(gh.prefilling)
-        gh.prefilling += self._admit(rep, g, room)
-        # prefill chunks (FIFO, one chunk per sequence per step, token budget)
-        budget = self.prefill_budget or (1 << 62)
-        chunks, finals = [], []
-        for sid in list(gh.prefilling):
-            s = self.seqs[sid]
-            L = len(s.prompt)
-            n = L - s.prefilled if self.chunk <= 0 else min(self.chunk, L - s.prefilled)
-            if chunks and n > budget:
-                break
-            budget -= n
-            a = s.prefilled
-            final = a + n == L
-            p = s.params
-            chunks.append(Chunk(sid, s.slot, a, s.prompt[a:a + n], final, p.temperature, p.top_k,
-                                p.greedy, s.seed))
-            s.prefilled += n
-            if final:
-                gh.prefilling.remove(sid)
-                finals.append(sid)
-                s.issued = 1
-                s.pos = L
-                s.sstep = 1
-        gp.chunks = chunks
-        # decode rows
-        gp.n = len(new_rows)
-        gp.b = _bucket(gp.n, self.cap)
-        if changed:
-            old_index = {sid: i for i, sid in enumerate(gh.rows)}
-            rows = []
-            for j, sid in enumerate(new_rows):
-                s = self.seqs[sid]
-                src = old_index[sid] if sid in old_index else prev.b + prev.finals.index(sid)
-                p = s.params
-                rows.append(Row(sid, s.slot, s.pos, p.temperature, p.top_k, p.greedy, s.seed,
-                                s.sstep, src))
-            gp.rows = rows
-        if gp.n:
-            top = max(self.seqs[sid].pos for sid in new_rows) + 1
-            gp.ctxb = min(-(-top // 256) * 256, self.eng.max_seq)
-            for sid in new_rows:  # this step issues one token per decode row
-                s = self.seqs[sid]
-                s.issued += 1
-                s.pos += 1
-                s.sstep += 1
-        gh.rows = new_rows
-        self.stats["max_rows"] = max(self.stats["max_rows"], gp.n)
-        if gp.b or finals:
-            gh.prev = Produced(gp.b, list(new_rows), finals, step=step)
-        if prev is not None:
-            self._register(rep, step, g, prev)
-        if not (gp.ret or gp.has_work):
-            return None
-        return gp
-
-    def _register(self, rep: int, step: int, g: int, prod: Produced) -> None:
-        self._expect[(rep, step, g)] = prod
-
     def build_step(self) -> Optional[List[StepPlan]]:
         """Plans of the next step for every replica, or None when idle."""
         self._take_new()
-        if not self.has_work():
+        if not self.core.has_work():
             return None
         s = self.step
         self.step += 1
-        plans = []
-        for rep in range(self.R):
-            gps = [gp for g in range(self.M) for gp in [self._group_plan(rep, g, s)] if gp is not None]
-            plans.append(StepPlan(step=s, groups=gps, replica=rep, timing=self.timing))
-        self.stats["steps"] += 1
+        per_rep, admitted = self.core.plan(s)
+        if admitted:
+            now = time.monotonic()
+            for sid in admitted:
+                self.meta[sid].req.t_start = now
+        plans = [StepPlan(step=s, groups=[self._group(go) for go in gos], replica=rep,
+                          timing=self.timing) for rep, gos in enumerate(per_rep)]
+        c = self.core
+        self.stats.update(steps=self.stats["steps"] + 1, joins=c.joins, leaves=c.leaves,
+                          max_rows=c.max_rows)
         if self.timing:
             self.step_log.append((s, any(gp.chunks for p in plans for gp in p.groups)))
         return plans
+
+    def _group(self, go) -> GroupPlan:
+        g, ret, n, b, ctxb, changed, chunks, rows = go
+        gp = GroupPlan(g, ret=ret, n=n, b=b, ctxb=ctxb)
+        meta = self.meta
+        for sid, slot, start, ln, final in chunks:
+            m = meta[sid]
+            p = m.req.params
+            gp.chunks.append(Chunk(sid, slot, start, m.req.prompt_ids[start:start + ln], final,
+                                   p.temperature, p.top_k, p.greedy, m.seed))
+        if changed:
+            out = []
+            for sid, slot, pos, sstep, src in rows:
+                m = meta[sid]
+                p = m.req.params
+                out.append(Row(sid, slot, pos, p.temperature, p.top_k, p.greedy, m.seed, sstep, src))
+            gp.rows = out
+        return gp
 
     # -- token readout -----------------------------------------------------------
     def on_readout(self, plan: StepPlan, gp: GroupPlan, ret: torch.Tensor) -> None:
         """Stage-0 worker callback: the token-return vector of group gp.g's
         previous item is in `ret` (in stream order): copy it to the host."""
-        prod = self._expect.pop((plan.replica, plan.step, gp.g))
+        key = (plan.replica, plan.step, gp.g)
         n = gp.ret
         if ret.is_cuda:
             host = torch.empty(n, dtype=torch.int32, pin_memory=True)
             host.copy_(ret[:n], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
-            self.readouts.append((plan.step, ev.query, ev.synchronize, host, prod))
+            self.readouts.append((plan.step, ev.query, ev.synchronize, host, key))
         else:
             host = ret[:n].clone()
-            self.readouts.append((plan.step, lambda: True, lambda: None, host, prod))
+            self.readouts.append((plan.step, lambda: True, lambda: None, host, key))
 
     def push_remote_readout(self, step: int, tokens: List[int], prod_key) -> None:
         """Replica > 0 readouts arrive over the control plane (dist + DP)."""
-        rep, st, g = prod_key
-        prod = self._expect.pop((rep, st, g))
         host = torch.tensor(tokens, dtype=torch.int32)
-        self.readouts.append((step, lambda: True, lambda: None, host, prod))
+        self.readouts.append((step, lambda: True, lambda: None, host, tuple(prod_key)))
 
     def poll(self, block_until_step: Optional[int] = None) -> None:
         """Process completed readouts (in order).  With block_until_step,
         wait for every readout of steps <= that one."""
         while self.readouts:
-            step, ready, sync, host, prod = self.readouts[0]
+            step, ready, sync, host, key = self.readouts[0]
             if not ready():
                 if block_until_step is None or step > block_until_step:
                     return
                 sync()
             self.readouts.popleft()
-            self._assign(host, prod)
+            self._assign(host, key)
 
-    def _assign(self, host: torch.Tensor, prod: Produced) -> None:
-        toks = host.tolist()
-        eos = self.eng.mcfg.eos_token_id
+    def _assign(self, host: torch.Tensor, key) -> None:
+        rep, step, g = key
+        events = self.core.assign(rep, step, g, host.tolist(), self.eng.mcfg.eos_token_id)
         now = time.monotonic()
-        for i, sid in enumerate(prod.rows):
-            self._give(self.seqs.get(sid), toks[i], eos, now)
-        for j, sid in enumerate(prod.finals):
-            self._give(self.seqs.get(sid), toks[prod.b + j], eos, now)
-        for sid in prod.release:
-            self._release(sid)
-
-    def _give(self, s: Optional[Seq], tok: int, eos: int, now: float) -> None:
-        if s is None or s.req.done or len(s.tokens) >= s.want:
-            return
-        if not s.tokens:
-            s.req.t_first = now
-        s.tokens.append(tok)
-        if s.params.stop_at_eos and tok == eos:
-            s.stop = True
-        if len(s.tokens) >= s.want or s.stop:
-            s.req.finish(list(s.tokens))
-
-    def _release(self, sid: int) -> None:
-        s = self.seqs.pop(sid, None)
-        if s is None:
-            return
-        if s.slot >= 0:
-            self.eng.slot_pools[s.rep].free([s.slot])
-        if not s.req.done:
-            s.req.finish(list(s.tokens))
+        meta = self.meta
+        for sid, tok, flags in events:
+            if flags & EV_RELEASE:
+                m = meta.pop(sid, None)
+                if m is not None and flags & EV_FINISH and not m.req.done:
+                    m.req.finish(list(m.tokens))
+                continue
+            m = meta.get(sid)
+            if m is None or m.req.done:
+                continue
+            if flags & EV_FIRST:
+                m.req.t_first = now
+            m.tokens.append(tok)
+            if flags & EV_FINISH:
+                m.req.finish(list(m.tokens))
 
     # -- failure -----------------------------------------------------------------
     def fail_all(self, err: BaseException) -> None:
-        for s in list(self.seqs.values()):
-            if not s.req.done:
-                s.req.finish(error=err)
-            if s.slot >= 0:
-                try:
-                    self.eng.slot_pools[s.rep].free([s.slot])
-                except Exception:  # pragma: no cover
-                    pass
-        self.seqs.clear()
-        self.waiting.clear()
+        for m in self.meta.values():
+            if not m.req.done:
+                m.req.finish(error=err)
+        self.meta.clear()
+        self.core.reset()
         self.readouts.clear()
-        self._expect.clear()
         with self._plock:
             pend = list(self._pending.values())
             self._pending.clear()
@@ -493,8 +589,6 @@ class Scheduler:
             pass
         for req in pend:
             req.finish(error=err)
-        self.groups = [[GroupHost() for _ in range(self.M)] for _ in range(self.R)]
-
 
 
 class Watchdog:
