@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--dp", type=int, default=int(os.environ.get("BENCH_DP", "1")),
                    help="pipeline replicas: N GPUs = (N/dp)-stage pipeline x dp (default 1: ppN)")
     p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),
-                   help="nccl (RCCL over xGMI) | gloo (host-staged, for rehearsals)")
+                   help="nccl (RCCL via torch.distributed) | rccl (native RCCL communicator, csrc/comm.cpp) | gloo (host-staged, for rehearsals)")
     p.add_argument("--loopback-stages", type=int, default=0,
                    help="rehearsal: run this many pipeline stages as threads on ONE GPU "
                         "(device-async loopback transport); --batch is then the total batch")

@@ -502,8 +502,11 @@ torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch:
 
 }  // namespace
 
+void lsd_register_comm(pybind11::module& m);  // csrc/comm.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "CDNA4 (gfx950) kernels for llm_sharding_demo_amd";
+  lsd_register_comm(m);
   m.def("linear", &linear);
   m.def("linear_f32", &linear_f32);
   m.def("linear_residual", &linear_residual);

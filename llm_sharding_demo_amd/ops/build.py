@@ -28,6 +28,8 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 KERNELS = ["gemm.hip", "gemv.hip", "norm.hip", "attention.hip", "sample.hip"]
+# host code of the extension: kernel bindings, native RCCL communicator
+HOST_SOURCES = ["bindings.cpp", "comm.cpp"]
 EXT_NAME = "_C"
 
 
@@ -83,16 +85,17 @@ def build(verbose: bool = False, force: bool = False) -> str:
         objs.append(obj)
         if force or not os.path.exists(obj) or not os.path.exists(stamp) or open(stamp).read() != sig:
             jobs.append(([HIPCC] + kflags + ["-c", src, "-o", obj], stamp, sig))
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.o")
     bflags = ["-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-DTORCH_EXTENSION_NAME={EXT_NAME}",
               "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-deprecated-declarations"] + inc
-    bsig = _hash([bsrc] + hdrs, " ".join(bflags))
-    bstamp = bobj + ".sha"
-    if force or not os.path.exists(bobj) or not os.path.exists(bstamp) or open(bstamp).read() != bsig:
-        jobs.append((["g++"] + bflags + ["-c", bsrc, "-o", bobj], bstamp, bsig))
-    objs.append(bobj)
+    for host_src in HOST_SOURCES:  # torch-extension host code (g++)
+        bsrc = os.path.join(CSRC, host_src)
+        bobj = os.path.join(BUILD, host_src.replace(".cpp", ".o"))
+        bsig = _hash([bsrc] + hdrs, " ".join(bflags))
+        bstamp = bobj + ".sha"
+        if force or not os.path.exists(bobj) or not os.path.exists(bstamp) or open(bstamp).read() != bsig:
+            jobs.append((["g++"] + bflags + ["-c", bsrc, "-o", bobj], bstamp, bsig))
+        objs.append(bobj)
 
     def do(job):
         cmd, stamp, sig = job
@@ -108,7 +111,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
         tmp = so + ".tmp"
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs +
              ["-o", tmp, f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
-              "-ltorch_python", "-ltorch_hip", f"-Wl,-rpath,{torch_lib}"], verbose)
+              "-ltorch_python", "-ltorch_hip", "-ldl", f"-Wl,-rpath,{torch_lib}"], verbose)
         os.replace(tmp, so)
     return so
 

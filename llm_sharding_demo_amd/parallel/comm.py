@@ -101,6 +101,8 @@ class _DistTransport(Transport):
     every replica has its own per-edge communicators, so replicas never
     share a link or an RCCL stream."""
 
+    EDGE_GROUPS = True  # a torch process group per pipeline edge
+
     def __init__(self, num_stages: int, replicas: int = 1):
         import torch.distributed as dist
 
@@ -118,10 +120,11 @@ class _DistTransport(Transport):
         for rep in range(R):
             base = rep * P
             for i in range(P - 1):
-                self.groups[f"r{rep}fwd{i}"] = dist.new_group([base + i, base + i + 1],
-                                                              backend=self._backend())
+                self.groups[f"r{rep}fwd{i}"] = (dist.new_group([base + i, base + i + 1], backend=self._backend())
+                                                if self.EDGE_GROUPS else None)
             if P > 1:
-                self.groups[f"r{rep}ret"] = dist.new_group([base + P - 1, base], backend=self._backend())
+                self.groups[f"r{rep}ret"] = (dist.new_group([base + P - 1, base], backend=self._backend())
+                                             if self.EDGE_GROUPS else None)
         self.ctrl = dist.new_group(list(range(P * R)), backend="gloo")
         # step plans (rank 0 -> every rank) and DP token readouts (replica
         # stage 0 -> rank 0) travel on their own gloo groups with no practical
@@ -236,6 +239,112 @@ class GlooTransport(_DistTransport):
         host = torch.empty(out.shape, dtype=out.dtype)
         work = self.dist.irecv(host, self._g(src), group=g)
         return Handle(out, work, post=lambda: out.copy_(host))
+
+
+class _EventWork:
+    """torch-Work-like wait(): the caller's stream waits on a HIP event."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self) -> None:
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+class RcclTransport(_DistTransport):
+    """Pipeline edges on the native RCCL communicator (csrc/comm.cpp).
+
+    Every edge (stage i -> i+1, and the token return P-1 -> 0) is its own
+    2-rank RCCL communicator with a dedicated comm stream. That stream keeps
+    the edge's operations in issue order on both ranks: the same ordering
+    ProcessGroupNCCL enforces, without which concurrent lanes could
+    interleave differently on the two GPUs.
+
+    A send or receive is made device-async by three event waits:
+    - the comm stream waits for the caller's stream, so the data or buffer
+      is ready;
+    - ncclSend / ncclRecv run on the comm stream;
+    - the caller's stream waits on the completion event in `.wait()`.
+    No host sync is involved.
+
+    The unique id of each edge is made by its first member and broadcast
+    over the gloo control group. Members then join in a fixed global order
+    (fwd0, fwd1, ..., ret), so the blocking inits complete left to right,
+    as in `warmup`."""
+
+    EDGE_GROUPS = False
+
+    def _backend(self) -> str:
+        return "gloo"  # control plane only; the data plane is native
+
+    def __init__(self, num_stages: int, replicas: int = 1):
+        super().__init__(num_stages, replicas)
+        from ..ops.hip import _load
+
+        self.C = _load()
+        self.comms: Dict[str, tuple] = {}  # edge -> (comm handle, comm stream, my index)
+        for name in self.groups:
+            members = self._members(name)
+            uid = self.C.rccl_unique_id() if self.grank == members[0] else None
+            uid = self.broadcast_object(uid, src=members[0])
+            if self.grank in members:
+                me = members.index(self.grank)
+                h = self.C.rccl_comm_init(2, me, uid)
+                self.comms[name] = (h, torch.cuda.Stream(), me)
+
+    def _edge(self, edge: str, src: int, dst: int):
+        name = f"r{self.replica}fwd{min(src, dst)}" if edge == "fwd" else f"r{self.replica}ret"
+        return self.comms[name]
+
+    def send(self, t, dst, edge):
+        h, cs, me = self._edge(edge, self.rank, dst)
+        if not t.is_contiguous():
+            t = t.contiguous()
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            self.C.rccl_send(h, t, 1 - me)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        t.record_stream(cs)
+        return SendHandle(_EventWork(ev))
+
+    def irecv(self, out, src, edge):
+        h, cs, me = self._edge(edge, src, self.rank)
+        buf = out if out.is_contiguous() else torch.empty(out.shape, dtype=out.dtype, device=out.device)
+        cs.wait_stream(torch.cuda.current_stream())  # the buffer's previous readers
+        with torch.cuda.stream(cs):
+            self.C.rccl_recv(h, buf, 1 - me)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        buf.record_stream(cs)
+        post = None if buf is out else (lambda: out.copy_(buf))
+        return Handle(out, _EventWork(ev), post=post)
+
+    def warmup(self, device) -> None:
+        """One exchange per edge, in the global edge order (checks the data)."""
+        for name, (h, cs, me) in self.comms.items():
+            src = self._members(name)[0]
+            buf = torch.full((4,), float(src), device=device)
+            if me == 0:
+                self.send(buf, self._stage_of(self._members(name)[1]),
+                          "ret" if name.endswith("ret") else "fwd").wait()
+            else:
+                got = torch.zeros(4, device=device)
+                self.irecv(got, self._stage_of(src), "ret" if name.endswith("ret") else "fwd").wait()
+                torch.cuda.synchronize(device)
+                if float(got[0].item()) != float(src):
+                    raise TransportError(f"warmup RCCL p2p on {name}: got {got[0].item()}, want {src}")
+        torch.cuda.synchronize(device)
+        self.barrier()
+
+    def _stage_of(self, grank: int) -> int:
+        return grank % self.P
+
+    def close(self) -> None:
+        torch.cuda.synchronize()
+        for h, _, _ in self.comms.values():
+            self.C.rccl_comm_destroy(h)
+        self.comms.clear()
 
 
 # ---------------------------------------------------------------------------
@@ -457,6 +566,10 @@ def init_distributed(backend: str, device_type: str, timeout_s: float = 600.0) -
 
 
 def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1) -> Transport:
+    if kind == "rccl":  # native communicator (csrc/comm.cpp)
+        t = RcclTransport(num_stages, replicas)
+        t.warmup(device)
+        return t
     if kind == "nccl":
         t = NcclTransport(num_stages, replicas)
         t.warmup(device)

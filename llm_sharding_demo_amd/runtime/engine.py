@@ -556,6 +556,8 @@ class Engine:
         if self.rank == 0:
             for t in self._tok_threads:
                 t.join(timeout=30)
+        self.transport.close()  # native RCCL communicators (no-op for torch groups)
+        self.transport.barrier()
         if dist.is_initialized():
             dist.destroy_process_group()
 
