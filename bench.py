@@ -43,7 +43,9 @@ def parse():
     p.add_argument("--prompt", type=int, default=128)
     p.add_argument("--gen", type=int, default=128)
     p.add_argument("--microbatches", type=int, default=int(os.environ.get("BENCH_MB", "0")),
-                   help="0 -> 2N: two microbatches (of --batch / 2 sequences) in flight per stage")
+                   help="0 -> auto: 2 groups per stage when decode reads more KV than weights "
+                        "(two lanes overlap one group's attention with the other's GEMMs), "
+                        "else 1 (weights read once per step)")
     p.add_argument("--dp", type=int, default=int(os.environ.get("BENCH_DP", "1")),
                    help="pipeline replicas: N GPUs = (N/dp)-stage pipeline x dp (default 1: ppN)")
     p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),
@@ -57,6 +59,22 @@ def parse():
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--seed", type=int, default=0)
     return p.parse_args()
+
+
+def auto_groups(args, P: int) -> int:
+    """Microbatch groups per replica: 2 per stage when a decode step reads more
+    KV cache than weights (GPT-2 XL at 512 x 192 positions: 629 vs 61 MB per
+    layer -- the two lanes overlap one group's attention with the other's
+    GEMMs: 46.5k vs 44.9k tok/s), otherwise 1 per stage so the weights are read
+    once per step (Llama-3 8B, 256 sequences: 201 vs 436 MB per layer, 21.4k vs
+    18.9k tok/s; profiles/r2_llama_microbatches.log)."""
+    from llm_sharding_demo_amd.config import get_model_config
+
+    mc = get_model_config(args.model)
+    ctx = args.prompt + args.gen // 2
+    kv = P * args.batch * ctx * mc.kv_bytes_per_token_per_layer()
+    weights = 2 * mc.block_params()
+    return 2 * P if kv > weights else P
 
 
 def main() -> int:
@@ -74,7 +92,7 @@ def main() -> int:
     if N % R:
         raise SystemExit(f"--gpus {N} is not a multiple of --dp {R}")
     P = N // R                      # pipeline stages per replica
-    M = args.microbatches or 2 * P  # microbatch groups per replica
+    M = args.microbatches or auto_groups(args, P)  # microbatch groups per replica
     B = N * args.batch              # global batch (weak scaling: fixed per GPU)
     Br = P * args.batch             # sequences per replica
     transport = args.transport
@@ -82,7 +100,7 @@ def main() -> int:
         if N != 1:
             raise SystemExit("--loopback-stages runs on one GPU")
         P = args.loopback_stages
-        M = args.microbatches or 2 * P
+        M = args.microbatches or auto_groups(args, P)
         transport = "loopback"
     cfg = EngineConfig(model_id=args.model, num_stages=P, dp_replicas=R, max_batch=Br,
                        max_seq_len=args.prompt + args.gen, device=args.device,

@@ -31,6 +31,7 @@ independent groups overlap on the GPU.
 from __future__ import annotations
 
 import contextlib
+import gc
 import os
 import threading
 import time
@@ -586,12 +587,22 @@ class StageWorker:
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with self._gate_released(), GPU_GATE.exclusive():
-            with torch.cuda.stream(s):
-                g.capture_begin(capture_error_mode="thread_local")
-                try:
-                    out = fn()
-                finally:
-                    g.capture_end()
+            # no garbage collection inside the capture: a collected object
+            # from an earlier session (a graph, an event, a communicator)
+            # would run HIP teardown calls that are illegal mid-capture
+            gc.collect()
+            was = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.stream(s):
+                    g.capture_begin(capture_error_mode="thread_local")
+                    try:
+                        out = fn()
+                    finally:
+                        g.capture_end()
+            finally:
+                if was:
+                    gc.enable()
         torch.cuda.current_stream(self.device).wait_stream(s)
         return g, out
 

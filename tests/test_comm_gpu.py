@@ -81,6 +81,10 @@ def test_rccl_pair_captured_in_graph(comm):
         g.replay()
         torch.cuda.synchronize()
         assert float(dst.min()) == v and float(dst.max()) == v
+    del g  # release the graph's RCCL resources now, not in a later test's capture
+    import gc
+
+    gc.collect()
 
 
 def test_rccl_rejects_bad_input(comm):

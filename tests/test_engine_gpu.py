@@ -142,7 +142,10 @@ def test_loopback_multi_stage_bit_identical(P):
     (stream waits on events, no host sync) produce the P = 1 tokens."""
     sp = SamplingParams(temperature=0.8, top_k=20, seed=7, max_new_tokens=10)
     prompts = [[i + 1, 2 * i + 3, 5] for i in range(12)]
-    one = _engine("gpt2-test").generate_ids(prompts, sp)
+    # same microbatch shapes on one stage: a 16-row group would run the
+    # split-K GEMM where 4-row groups run the GEMV (equal to bf16 rounding,
+    # not bit-equal -- tools/check_m1.py)
+    one = _engine("gpt2-test", num_microbatches=2 * P).generate_ids(prompts, sp)
     e = Engine(EngineConfig(model_id="gpt2-test", num_stages=P, max_batch=16, device="cuda",
                             num_microbatches=2 * P, transport="loopback"))
     from llm_sharding_demo_amd.parallel.comm import LoopbackTransport
