@@ -46,3 +46,20 @@ def test_bench_json_contract(n, dp):
     # value is the whole-job token rate over the timed steps
     toks = d["config"]["global_batch"] * d["config"]["gen_tokens"]
     assert d["value"] == pytest.approx(toks / (d["ms_per_step"] / 1e3), rel=0.02)
+
+
+def test_auto_microbatch_groups():
+    """bench.py default groups: 2 per stage when a decode step reads more KV
+    than weights (GPT-2 XL headline), 1 per stage otherwise (Llama-3 8B)."""
+    import importlib.util
+    import types
+
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    a = lambda m, n: types.SimpleNamespace(model=m, batch=n, prompt=128, gen=128)  # noqa: E731
+    assert b.auto_groups(a("gpt2-xl", 512), 1) == 2
+    assert b.auto_groups(a("gpt2-xl", 512), 8) == 16
+    assert b.auto_groups(a("gpt2-xl", 1), 1) == 1
+    assert b.auto_groups(a("llama-3-8b", 256), 1) == 1
+    assert b.auto_groups(a("llama-3-8b", 256), 4) == 8  # 1024 sequences per stage: KV-bound again
