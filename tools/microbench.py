@@ -416,6 +416,29 @@ def stamps_p8(M=65536, N=6400, K=1600, act=1):
     print(json.dumps(row), flush=True)
 
 
+def bench_lmhead_kinds(M=256, N=50304, K=1600):
+    """Decode vocab projection at M rows: 256x256 phase-pipelined tiles vs the
+    128x128 tiled kernel (2 blocks/CU) vs hipBLASLt; rotating weights."""
+    ws = rotating(lambda: torch.randn(N, K, device=DEV).bfloat16(), N * K * 2)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    it = [0]
+
+    def run():
+        w = ws[it[0] % len(ws)]
+        it[0] += 1
+        C.linear_f32(a, w, True, 1, None)
+    for name, bm in (("p8", 1), ("tiled128", 1 << 30)):
+        C.gemm_set_big_min(bm)
+        report(f"lmhead_{name} M={M} N={N} K={K}", timeit(run), N * K * 2)
+    C.gemm_set_big_min(160)
+
+    def ref():
+        w = ws[it[0] % len(ws)]
+        it[0] += 1
+        torch.matmul(a, w.t())
+    report(f"lmhead_hipblaslt M={M} N={N} K={K}", timeit(ref), N * K * 2)
+
+
 def stamps_gemm(M, N, K, splits, act=0, label=""):
     """Per-workgroup phase timeline of one decode-GEMM launch (diagnostic)."""
     w = torch.randn(N, K, device=DEV).bfloat16()
@@ -575,6 +598,10 @@ def main():
     if "p8stamps" in which:
         stamps_p8()
         stamps_p8(N=1600, K=6400, act=0)
+    if "lmk" in which:
+        for M in (256, 512):
+            bench_lmhead_kinds(M)
+        bench_lmhead_kinds(256, 128256, 4096)
     if "sample" in which:
         for B in (1, 64, 256):
             for g in (True, False):
