@@ -373,6 +373,13 @@ static int g_attn_max_wg = 0;  // 0: one workgroup per (sequence, kv head)
 extern "C" void lsd_attn_set_max_wg(int v) { g_attn_max_wg = v; }
 static int g_attn_small_waves = 8;  // waves per block for small decode batches (4, 8, 16)
 extern "C" void lsd_attn_set_small_waves(int v) { g_attn_small_waves = v; }
+// waves per block for full decode batches, by head dim (4 or 8); 8 also
+// requests V with K (lsd_attn_set_large_waves: tuning / A/B)
+static int g_attn_large_waves64 = 4, g_attn_large_waves128 = 4;
+extern "C" void lsd_attn_set_large_waves(int hd, int v) {
+  if (hd == 64) g_attn_large_waves64 = v == 8 ? 8 : 4;
+  else g_attn_large_waves128 = v == 8 ? 8 : 4;
+}
 
 extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
                                       const int* seq_slots, const int* qpos, bf16* out, long ldo,
@@ -385,7 +392,8 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
   const int gx = g_attn_max_wg > 0 ? (n_items < g_attn_max_wg ? n_items : g_attn_max_wg) : n_items;
   // fewer blocks than half the CUs: wider blocks (g_attn_small_waves waves),
   // K and V of an item requested in one round of loads
-  const int sw = (long)gx * splits <= 128 ? g_attn_small_waves : 0;
+  const int sw = (long)gx * splits <= 128 ? g_attn_small_waves
+                                           : ((hd == 64 ? g_attn_large_waves64 : g_attn_large_waves128) == 8 ? 8 : 0);
   dim3 grid(gx, splits);
 #define LSD_DEC(HDV, GV)                                                                        \
   if (hd == HDV && G == GV) {                                                                   \

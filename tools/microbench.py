@@ -439,6 +439,56 @@ def bench_lmhead_kinds(M=256, N=50304, K=1600):
     report(f"lmhead_hipblaslt M={M} N={N} K={K}", timeit(ref), N * K * 2)
 
 
+def bench_llama_decode_kinds(M=256):
+    """Llama-3 8B decode GEMMs at M rows under each tiled-kernel choice:
+    128x128 double buffer, LDS ring 128x64 / 128x128, phase-pipelined 256x256."""
+    H, F = 4096, 14336
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    shapes = [("qkv", 6144, H, 0), ("gate_up", 2 * F, H, 2), ("o_proj", H, H, -1), ("down", H, F, -1)]
+    for name, N, K, act in shapes:
+        ws = rotating(lambda N=N, K=K: torch.randn(N, K, device=DEV).bfloat16(), N * K * 2)
+        a = torch.randn(M, K, device=DEV).bfloat16()
+        x = torch.randn(M, N, device=DEV)
+        for kind, t3, tn, bm in (("dbuf128", 0, 128, 1 << 30), ("ring64", 1 << 30, 64, 1 << 30),
+                                 ("ring128", 1 << 30, 128, 1 << 30), ("p8", 0, 64, 1)):
+            C.gemm_set_tiled3_max(t3)
+            C.gemm_set_ring_tn(tn)
+            C.gemm_set_big_min(bm)
+            it = [0]
+
+            def run(ws=ws, a=a, x=x, act=act, it=it, N=N):
+                w = ws[it[0] % len(ws)]
+                it[0] += 1
+                if act < 0:
+                    C.linear_residual(a, w, None, x, 1, True, cnt, False)
+                else:
+                    C.linear(a, w, None, act, True, 1, cnt)
+            report(f"llama_{name}_{kind} M={M} N={N} K={K}", timeit(run, iters=20), N * K * 2)
+    C.gemm_set_tiled3_max(512)
+    C.gemm_set_ring_tn(0)
+    C.gemm_set_big_min(160)
+
+
+def bench_llama_sk(M=256):
+    """Llama-3 8B decode GEMMs on the split-K decode kernel (W straight to
+    VGPRs, last-arriver combine) at several splits."""
+    H, F = 4096, 14336
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+    for name, N, K, act in (("qkv", 6144, H, 0), ("gate_up", 2 * F, H, 2), ("o_proj", H, H, 0), ("down", H, F, 0)):
+        ws = rotating(lambda N=N, K=K: torch.randn(N, K, device=DEV).bfloat16(), N * K * 2)
+        a = torch.randn(M, K, device=DEV).bfloat16()
+        for S in (1, 2, 4, 8):
+            if K // 32 // S < 2:
+                continue
+            it = [0]
+
+            def run(ws=ws, a=a, act=act, it=it, S=S):
+                w = ws[it[0] % len(ws)]
+                it[0] += 1
+                C.linear(a, w, None, act, False, S, cnt)
+            report(f"llama_{name}_sk M={M} N={N} K={K} S={S}", timeit(run, iters=20), N * K * 2)
+
+
 def stamps_gemm(M, N, K, splits, act=0, label=""):
     """Per-workgroup phase timeline of one decode-GEMM launch (diagnostic)."""
     w = torch.randn(N, K, device=DEV).bfloat16()
@@ -602,6 +652,20 @@ def main():
         for M in (256, 512):
             bench_lmhead_kinds(M)
         bench_lmhead_kinds(256, 128256, 4096)
+    if "attnw" in which:  # full-batch decode attention: 4 vs 8 waves per block
+        for hd, nh, nkv in ((128, 32, 8), (64, 25, 25)):
+            for B, ctx in ((256, 160), (256, 192), (128, 192), (512, 192)):
+                for wv in (4, 8):
+                    C.attn_set_large_waves(hd, wv)
+                    print("waves", wv, flush=True)
+                    bench_attn_decode(B, nh, nkv, hd, ctx)
+            C.attn_set_large_waves(hd, 4)
+    if "llamak" in which:
+        for M in (256, 128):
+            bench_llama_decode_kinds(M)
+    if "llamask" in which:
+        for M in (256, 128):
+            bench_llama_sk(M)
     if "sample" in which:
         for B in (1, 64, 256):
             for g in (True, False):
