@@ -28,6 +28,7 @@ void lsd_gemm_set_ring_fill(int v);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
 void lsd_attn_set_large_waves(int hd, int v);
+void lsd_attn_set_mfma_min(int v);
 int lsd_gemm_sk_rows(int M, int N, int S);
 int lsd_gemm_sk_rblocks(int M, int N, int S);
 int lsd_gemm_sk_nw(int M, int epi);
@@ -538,6 +539,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // decode attention: waves per block when the batch has few (sequence, head) items
   m.def("attn_set_small_waves", [](int64_t v) { lsd_attn_set_small_waves((int)v); });
   m.def("attn_set_large_waves", [](int64_t hd, int64_t v) { lsd_attn_set_large_waves((int)hd, (int)v); });
+  // grouped-query MFMA decode attention from this many (sequence, kv head) items (0 = off)
+  m.def("attn_set_mfma_min", [](int64_t v) { lsd_attn_set_mfma_min((int)v); });
   // decode GEMM: rows per row block (M above it runs as several row blocks)
   m.def("gemm_set_sk_rows", [](int64_t v) { lsd_gemm_set_sk_rows((int)v); });
   m.def("gemm_sk_rblocks", [](int64_t M, int64_t N, int64_t S) { return lsd_gemm_sk_rblocks((int)M, (int)N, (int)S); });

@@ -365,6 +365,152 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decode, grouped-query heads on MFMA: one wave per (sequence, kv head)
+// ---------------------------------------------------------------------------
+// The VALU decode kernel above spends per key G x HD multiply-adds on the
+// scores and as many on P.V, plus a 16-lane reduction per score: with
+// Llama-3's G = 4 query heads of HD = 128 per kv head it is VALU-bound (about
+// 3.6 TB/s of KV at 256 sequences against the 6.3 TB/s HBM floor).  Here the
+// G queries of one kv head are the columns of an MFMA tile, the prefill
+// kernel's swapped-operand scheme with a key tile instead of a query tile:
+//   S^T[key][q] = K[key][d] . Q^T[d][q]      (16 keys x 16 columns, G valid)
+//   O^T[d][q]  += V^T[d][key] . P^T[key][q]  (P^T straight from S^T's registers,
+//                                             V^T via ds_read_b64_tr_b16)
+// 32-key tiles of K and V are streamed with non-temporal 16-byte loads into
+// registers (the next tile's loads in flight under the current tile's math),
+// then staged through this wave's own LDS region for the fragment reads.
+// Waves are independent: no block barrier.  The math is ~2% of the HBM time
+// of the KV stream, so the kernel runs at the KV roofline.
+template <int HD, int G>
+__global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
+    const bf16* __restrict__ q, long ldq, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const int* __restrict__ seq_slots, const int* __restrict__ qpos, bf16* out, long ldo, int n_kv,
+    int max_seq, float scale_log2, int n_items) {
+  static_assert(G >= 1 && G <= 16, "G query heads per kv head fit one MFMA column tile");
+  constexpr int KT = 32;             // keys per tile
+  constexpr int LDR = HD + 8;        // padded LDS row (elements): +16 B
+  constexpr int CPR = HD / 8;        // 16-B chunks per key row
+  constexpr int CH = KT * CPR / 64;  // chunks per lane per tile (per K and per V)
+  __shared__ __attribute__((aligned(16))) bf16 lds[4][2][KT * LDR];
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int item = blockIdx.x * 4 + w;
+  if (item >= n_items) return;  // waves are independent: no barriers below
+  bf16* ks = lds[w][0];
+  bf16* vs = lds[w][1];
+  const int b = item / n_kv, kvh = item % n_kv;
+  const int ctx = qpos[b] + 1;
+  const long base = ((long)seq_slots[b] * n_kv + kvh) * (long)max_seq * HD;
+  const int r = lane & 15, g = lane >> 4;
+
+  // Q^T fragments: column r = query head kvh * G + r (zero columns past G)
+  bf16x8 qf[HD / 32];
+#pragma unroll
+  for (int kk = 0; kk < HD / 32; ++kk) {
+    bf16x8 z = {};
+    qf[kk] = r < G ? ld8(q + (long)b * ldq + (long)(kvh * G + r) * HD + kk * 32 + g * 8) : z;
+  }
+  f32x4 o[HD / 16];
+#pragma unroll
+  for (int di = 0; di < HD / 16; ++di) o[di] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = NEG, lsum = 0.f;
+
+  const int ntile = (ctx + KT - 1) / KT;
+  bf16x8 kreg[CH], vreg[CH];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = lane + c * 64;
+      const int key = min(t * KT + idx / CPR, ctx - 1);
+      const long off = base + (long)key * HD + (idx % CPR) * 8;
+      kreg[c] = LSD_KV_LOAD(kc + off);
+      vreg[c] = LSD_KV_LOAD(vc + off);
+    }
+  };
+  load_tile(0);
+  for (int t = 0; t < ntile; ++t) {
+    // the previous tile's fragment reads must be done before the overwrite
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = lane + c * 64;
+      st8(ks + (idx / CPR) * LDR + (idx % CPR) * 8, kreg[c]);
+      st8(vs + (idx / CPR) * LDR + (idx % CPR) * 8, vreg[c]);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    if (t + 1 < ntile) load_tile(t + 1);  // in flight under this tile's math
+
+    f32x4 sacc[2];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      sacc[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < HD / 32; ++kk) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (ni * 16 + r) * LDR + kk * 32 + g * 8);
+        sacc[ni] = mfma16(kf, qf[kk], sacc[ni]);
+      }
+    }
+    float tmax = NEG;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = t * KT + ni * 16 + 4 * g + i;
+        const float sv = key < ctx ? sacc[ni][i] * scale_log2 : NEG;
+        sacc[ni][i] = sv;
+        tmax = fmaxf(tmax, sv);
+      }
+    tmax = fmaxf(tmax, wave_xchg<16>(tmax));
+    tmax = fmaxf(tmax, wave_xchg<32>(tmax));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = exp2f(sacc[ni][i] - mn);
+        sacc[ni][i] = p;
+        ps += p;
+      }
+    lsum = lsum * alpha + ps;
+#pragma unroll
+    for (int di = 0; di < HD / 16; ++di) o[di] *= alpha;
+    // O^T += V^T . P^T over the 32 keys: k-slot j of group g <-> key 4g + j
+    // (j < 4), 16 + 4g + (j - 4) (j >= 4)
+    bf16x8 pf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pf[j] = f2bf(sacc[0][j]);
+      pf[4 + j] = f2bf(sacc[1][j]);
+    }
+    const int r0 = 4 * g + (r >> 2);
+#pragma unroll
+    for (int di = 0; di < HD / 16; ++di) {
+      const int col = di * 16 + 4 * (r & 3);
+      const bf16x4 lo = ds_read_tr(vs + r0 * LDR + col);
+      const bf16x4 hi = ds_read_tr(vs + (r0 + 16) * LDR + col);
+      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[di] = mfma16(vf, pf, o[di]);
+    }
+  }
+  lsum += wave_xchg<16>(lsum);
+  lsum += wave_xchg<32>(lsum);
+  if (r < G) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* op = out + (long)b * ldo + (long)(kvh * G + r) * HD;
+#pragma unroll
+    for (int di = 0; di < HD / 16; ++di) {
+      bf16x4 rr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rr[i] = f2bf(o[di][i] * inv);
+      st4(op + di * 16 + 4 * g, rr);
+    }
+  }
+}
+
 }  // namespace lsd
 
 using namespace lsd;
@@ -376,6 +522,11 @@ extern "C" void lsd_attn_set_small_waves(int v) { g_attn_small_waves = v; }
 // waves per block for full decode batches, by head dim (4 or 8); 8 also
 // requests V with K (lsd_attn_set_large_waves: tuning / A/B)
 static int g_attn_large_waves64 = 4, g_attn_large_waves128 = 4;
+// grouped-query decode on MFMA (attn_decode_mfma_kernel) for HD = 128,
+// 2 <= G <= 16, one split, at least this many (sequence, kv head) items;
+// 0 = off (lsd_attn_set_mfma_min)
+static int g_attn_mfma_min = 256;
+extern "C" void lsd_attn_set_mfma_min(int v) { g_attn_mfma_min = v; }
 extern "C" void lsd_attn_set_large_waves(int hd, int v) {
   if (hd == 64) g_attn_large_waves64 = v == 8 ? 8 : 4;
   else g_attn_large_waves128 = v == 8 ? 8 : 4;
@@ -392,6 +543,19 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
   const int gx = g_attn_max_wg > 0 ? (n_items < g_attn_max_wg ? n_items : g_attn_max_wg) : n_items;
   // fewer blocks than half the CUs: wider blocks (g_attn_small_waves waves),
   // K and V of an item requested in one round of loads
+  if (g_attn_mfma_min > 0 && hd == 128 && splits == 1 && g_attn_max_wg == 0 && n_items >= g_attn_mfma_min) {
+    const dim3 mgrid((n_items + 3) / 4);
+#define LSD_DEC_MFMA(GV)                                                                        \
+  if (G == GV) {                                                                                \
+    hipLaunchKernelGGL((attn_decode_mfma_kernel<128, GV>), mgrid, dim3(256), 0, st, q, ldq, kc, \
+                       vc, seq_slots, qpos, out, ldo, n_kv, max_seq, scale_log2, n_items);      \
+    return hipGetLastError();                                                                   \
+  }
+    LSD_DEC_MFMA(2)
+    LSD_DEC_MFMA(4)
+    LSD_DEC_MFMA(8)
+#undef LSD_DEC_MFMA
+  }
   const int sw = (long)gx * splits <= 128 ? g_attn_small_waves
                                            : ((hd == 64 ? g_attn_large_waves64 : g_attn_large_waves128) == 8 ? 8 : 0);
   dim3 grid(gx, splits);

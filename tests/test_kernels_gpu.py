@@ -325,6 +325,36 @@ def _attention_decode_case(C, hd, nh, n_kv, splits, B=5):
     close(o.reshape(B, nh, hd), o_ref, 2e-2)
 
 
+@pytest.mark.parametrize("nh,n_kv", [(32, 8), (16, 8), (64, 8)])
+@pytest.mark.parametrize("B", [40, 3])
+def test_attention_decode_mfma_grouped(C, nh, n_kv, B):
+    """Grouped-query decode on MFMA (HD 128, G = 2 / 4 / 8 query heads per kv
+    head), forced on for any batch: positions at 32-key tile edges, against
+    the fp32 reference and the VALU kernel."""
+    hd, slots, S = 128, max(B, 8), 300
+    kc, vc = bf(slots, n_kv, S, hd, seed=26), bf(slots, n_kv, S, hd, seed=27)
+    q = bf(B, nh * hd, seed=28)
+    g = torch.Generator().manual_seed(B + nh)
+    seq_slots = torch.randperm(slots, generator=g)[:B].int().to(DEV)
+    edge = [0, 30, 31, 32, 63, 64, 95, 299]
+    pos = torch.tensor([edge[i] if i < len(edge) else int(torch.randint(0, S, (1,), generator=g))
+                        for i in range(B)], dtype=torch.int32, device=DEV)
+    cu = torch.arange(B + 1, dtype=torch.int32)
+    o_ref = ref.attention(q.reshape(B, nh, hd).cpu(), kc.cpu(), vc.cpu(), seq_slots.cpu(), pos.cpu(), cu)
+    C.attn_set_mfma_min(1)
+    try:
+        o = C.attn_decode(q, kc, vc, seq_slots, pos, nh, 1)
+    finally:
+        C.attn_set_mfma_min(256)
+    close(o.reshape(B, nh, hd), o_ref, 2e-2)
+    C.attn_set_mfma_min(0)
+    try:
+        o_valu = C.attn_decode(q, kc, vc, seq_slots, pos, nh, 1)
+    finally:
+        C.attn_set_mfma_min(256)
+    close(o, o_valu, 2e-2)
+
+
 @pytest.mark.parametrize("hd,nh,n_kv", [(64, 4, 4), (128, 8, 2)])
 def test_attention_prefill_ragged_chunked(C, hd, nh, n_kv):
     from llm_sharding_demo_amd.ops.hip import prefill_tiles

@@ -652,6 +652,13 @@ def main():
         for M in (256, 512):
             bench_lmhead_kinds(M)
         bench_lmhead_kinds(256, 128256, 4096)
+    if "attnm" in which:  # grouped-query decode: MFMA kernel vs VALU kernel
+        for B, ctx in ((256, 160), (256, 192), (128, 192), (512, 192), (64, 1024)):
+            for mm in (256, 0):
+                C.attn_set_mfma_min(mm)
+                print("mfma_min", mm, flush=True)
+                bench_attn_decode(B, 32, 8, 128, ctx)
+        C.attn_set_mfma_min(256)
     if "attnw" in which:  # full-batch decode attention: 4 vs 8 waves per block
         for hd, nh, nkv in ((128, 32, 8), (64, 25, 25)):
             for B, ctx in ((256, 160), (256, 192), (128, 192), (512, 192)):
