@@ -63,14 +63,21 @@ def parse():
 
 def auto_groups(args, P: int) -> int:
     """Microbatch groups per replica: 2 per stage when a decode step reads more
-    KV cache than weights (GPT-2 XL at 512 x 192 positions: 629 vs 61 MB per
-    layer -- the two lanes overlap one group's attention with the other's
-    GEMMs: 46.5k vs 44.9k tok/s), otherwise 1 per stage so the weights are read
-    once per step (Llama-3 8B, 256 sequences: 201 vs 436 MB per layer, 21.4k vs
-    18.9k tok/s; profiles/r2_llama_microbatches.log)."""
+    KV cache than weights AND the attention runs on the VALU decode kernel
+    (GPT-2 XL at 512 x 192 positions: 629 vs 61 MB per layer -- the two lanes
+    overlap one group's attention with the other's GEMMs: 46.5k vs 44.9k
+    tok/s), otherwise 1 per stage so the weights are read once per step
+    (Llama-3 8B, 256 sequences: 201 vs 436 MB per layer, 21.4k vs 18.9k tok/s;
+    profiles/r2_llama_microbatches.log).  Grouped-query attention on MFMA
+    (head_dim 128, 2-8 query heads per kv head) streams the KV at the HBM
+    roofline, so there is nothing to overlap: Llama-3 8B at 32 x 4K positions
+    (545 vs 436 MB per layer) 1405 vs 1272 tok/s on 1 group
+    (profiles/r2_long_context.log)."""
     from llm_sharding_demo_amd.config import get_model_config
 
     mc = get_model_config(args.model)
+    if mc.head_dim == 128 and mc.n_heads // mc.n_kv_heads in (2, 4, 8):
+        return P
     ctx = args.prompt + args.gen // 2
     kv = P * args.batch * ctx * mc.kv_bytes_per_token_per_layer()
     weights = 2 * mc.block_params()

@@ -385,8 +385,9 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
 template <int HD, int G>
 __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, long ldq, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
-    const int* __restrict__ seq_slots, const int* __restrict__ qpos, bf16* out, long ldo, int n_kv,
-    int max_seq, float scale_log2, int n_items) {
+    const int* __restrict__ seq_slots, const int* __restrict__ qpos, bf16* out, long ldo,
+    float* part_o, float* part_ml, int n_kv, int max_seq, int splits, float scale_log2,
+    int n_items) {
   static_assert(G >= 1 && G <= 16, "G query heads per kv head fit one MFMA column tile");
   constexpr int KT = 32;             // keys per tile
   constexpr int LDR = HD + 8;        // padded LDS row (elements): +16 B
@@ -400,6 +401,9 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
   bf16* vs = lds[w][1];
   const int b = item / n_kv, kvh = item % n_kv;
   const int ctx = qpos[b] + 1;
+  // split blockIdx.y of the context (long contexts: more waves than items)
+  const int per = (ctx + splits - 1) / splits;
+  const int k_lo = blockIdx.y * per, k_hi = min(ctx, k_lo + per);
   const long base = ((long)seq_slots[b] * n_kv + kvh) * (long)max_seq * HD;
   const int r = lane & 15, g = lane >> 4;
 
@@ -415,19 +419,19 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
   for (int di = 0; di < HD / 16; ++di) o[di] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = NEG, lsum = 0.f;
 
-  const int ntile = (ctx + KT - 1) / KT;
+  const int ntile = k_hi > k_lo ? (k_hi - k_lo + KT - 1) / KT : 0;
   bf16x8 kreg[CH], vreg[CH];
   auto load_tile = [&](int t) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = lane + c * 64;
-      const int key = min(t * KT + idx / CPR, ctx - 1);
+      const int key = min(k_lo + t * KT + idx / CPR, k_hi - 1);
       const long off = base + (long)key * HD + (idx % CPR) * 8;
       kreg[c] = LSD_KV_LOAD(kc + off);
       vreg[c] = LSD_KV_LOAD(vc + off);
     }
   };
-  load_tile(0);
+  if (ntile > 0) load_tile(0);
   for (int t = 0; t < ntile; ++t) {
     // the previous tile's fragment reads must be done before the overwrite
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -456,8 +460,8 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int key = t * KT + ni * 16 + 4 * g + i;
-        const float sv = key < ctx ? sacc[ni][i] * scale_log2 : NEG;
+        const int key = k_lo + t * KT + ni * 16 + 4 * g + i;
+        const float sv = key < k_hi ? sacc[ni][i] * scale_log2 : NEG;
         sacc[ni][i] = sv;
         tmax = fmaxf(tmax, sv);
       }
@@ -498,7 +502,16 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
   }
   lsum += wave_xchg<16>(lsum);
   lsum += wave_xchg<32>(lsum);
-  if (r < G) {
+  if (r < G && splits > 1) {  // unnormalised partial for attn_decode_combine_kernel
+    const long pi = ((long)b * n_kv * G + kvh * G + r) * splits + blockIdx.y;
+    float* po = part_o + pi * HD;
+#pragma unroll
+    for (int di = 0; di < HD / 16; ++di) *reinterpret_cast<f32x4*>(po + di * 16 + 4 * g) = o[di];
+    if (g == 0) {
+      part_ml[pi * 2] = m;
+      part_ml[pi * 2 + 1] = lsum;
+    }
+  } else if (r < G) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16* op = out + (long)b * ldo + (long)(kvh * G + r) * HD;
 #pragma unroll
@@ -523,13 +536,27 @@ extern "C" void lsd_attn_set_small_waves(int v) { g_attn_small_waves = v; }
 // requests V with K (lsd_attn_set_large_waves: tuning / A/B)
 static int g_attn_large_waves64 = 4, g_attn_large_waves128 = 4;
 // grouped-query decode on MFMA (attn_decode_mfma_kernel) for HD = 128,
-// 2 <= G <= 16, one split, at least this many (sequence, kv head) items;
-// 0 = off (lsd_attn_set_mfma_min)
+// G in {2, 4, 8}, at least this many waves ((sequence, kv head) items x
+// context splits); 0 = off (lsd_attn_set_mfma_min).  ops/hip.py picks the
+// splits so that long contexts reach it with few sequences.
 static int g_attn_mfma_min = 256;
 extern "C" void lsd_attn_set_mfma_min(int v) { g_attn_mfma_min = v; }
 extern "C" void lsd_attn_set_large_waves(int hd, int v) {
   if (hd == 64) g_attn_large_waves64 = v == 8 ? 8 : 4;
   else g_attn_large_waves128 = v == 8 ? 8 : 4;
+}
+
+static hipError_t attn_decode_combine(const float* part_o, const float* part_ml, bf16* out, long ldo,
+                                      int B, int nh, int hd, int splits, hipStream_t st) {
+  if (splits > 1) {
+    if (hd == 64)
+      hipLaunchKernelGGL((attn_decode_combine_kernel<64>), dim3(B * nh), dim3(64), 0, st, part_o,
+                         part_ml, out, ldo, nh, splits);
+    else
+      hipLaunchKernelGGL((attn_decode_combine_kernel<128>), dim3(B * nh), dim3(64), 0, st, part_o,
+                         part_ml, out, ldo, nh, splits);
+  }
+  return hipGetLastError();
 }
 
 extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
@@ -543,13 +570,14 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
   const int gx = g_attn_max_wg > 0 ? (n_items < g_attn_max_wg ? n_items : g_attn_max_wg) : n_items;
   // fewer blocks than half the CUs: wider blocks (g_attn_small_waves waves),
   // K and V of an item requested in one round of loads
-  if (g_attn_mfma_min > 0 && hd == 128 && splits == 1 && g_attn_max_wg == 0 && n_items >= g_attn_mfma_min) {
-    const dim3 mgrid((n_items + 3) / 4);
+  if (g_attn_mfma_min > 0 && hd == 128 && g_attn_max_wg == 0 && (long)n_items * splits >= g_attn_mfma_min) {
+    const dim3 mgrid((n_items + 3) / 4, splits);
 #define LSD_DEC_MFMA(GV)                                                                        \
   if (G == GV) {                                                                                \
     hipLaunchKernelGGL((attn_decode_mfma_kernel<128, GV>), mgrid, dim3(256), 0, st, q, ldq, kc, \
-                       vc, seq_slots, qpos, out, ldo, n_kv, max_seq, scale_log2, n_items);      \
-    return hipGetLastError();                                                                   \
+                       vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq, splits,   \
+                       scale_log2, n_items);                                                    \
+    return attn_decode_combine(part_o, part_ml, out, ldo, B, nh, hd, splits, st);              \
   }
     LSD_DEC_MFMA(2)
     LSD_DEC_MFMA(4)
@@ -585,15 +613,7 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
 #undef LSD_DEC
   return hipErrorInvalidValue;
 combine:
-  if (splits > 1) {
-    if (hd == 64)
-      hipLaunchKernelGGL((attn_decode_combine_kernel<64>), dim3(B * nh), dim3(64), 0, st, part_o,
-                         part_ml, out, ldo, nh, splits);
-    else
-      hipLaunchKernelGGL((attn_decode_combine_kernel<128>), dim3(B * nh), dim3(64), 0, st, part_o,
-                         part_ml, out, ldo, nh, splits);
-  }
-  return hipGetLastError();
+  return attn_decode_combine(part_o, part_ml, out, ldo, B, nh, hd, splits, st);
 }
 
 extern "C" hipError_t lsd_attn_prefill(const bf16* q, long ldq, const bf16* kc, const bf16* vc,

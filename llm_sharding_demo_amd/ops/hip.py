@@ -111,6 +111,16 @@ class HipBackend(Backend):
     GEMV_MAX_M = int(os.environ.get("LSD_GEMV_MAX_M", "8"))
     GEMV_NORM_MAX_M = int(os.environ.get("LSD_GEMV_NORM_MAX_M", "2"))
     TARGET_BLOCKS = 512  # >> 256 CUs so every CU streams
+    # Grouped-query decode attention on MFMA (attention.hip
+    # attn_decode_mfma_kernel, one wave per (sequence, kv head, split)): taken
+    # at >= ATTN_MFMA_MIN waves (the kernel's own default).  Fewer than
+    # ATTN_MFMA_SPLIT_BELOW items (long contexts, few sequences) split the
+    # context towards ATTN_MFMA_WAVES waves, >= 512 keys per split.  1024
+    # waves measured best (Llama-3 8B shapes, 2K-8K contexts: 1.3-1.45x the
+    # split VALU kernel; profiles/r2_long_context.log)
+    ATTN_MFMA_MIN = 256
+    ATTN_MFMA_SPLIT_BELOW = 1024
+    ATTN_MFMA_WAVES = int(os.environ.get("LSD_ATTN_MFMA_WAVES", "1024"))
     # decode GEMM: aim for this many workgroups (column tiles x k-splits)
     # decode (split-K, last-arriver) GEMM up to this many rows (above 128 as
     # row blocks of <= 128 sharing each W tile); tiled above.  256-row decode
@@ -319,14 +329,26 @@ class HipBackend(Backend):
                                  mcfg.q_size, mcfg.kv_size, mcfg.head_dim, self._rope,
                                  tiled, splits, self.counters)
 
+    @classmethod
+    def decode_attn_splits(cls, B: int, nh: int, n_kv: int, hd: int, max_ctx: int) -> int:
+        """Context splits of a decode attention launch (a graph-captured
+        property: max_ctx is the captured context bucket)."""
+        G, items = nh // n_kv, B * n_kv
+        if hd == 128 and G in (2, 4, 8):
+            ms = 1
+            if items < cls.ATTN_MFMA_SPLIT_BELOW:
+                ms = max(1, min(math.ceil(cls.ATTN_MFMA_WAVES / items), math.ceil(max_ctx / 512), 256))
+            if items * ms >= cls.ATTN_MFMA_MIN:
+                return ms
+        if items < cls.TARGET_BLOCKS:
+            return min(math.ceil(cls.TARGET_BLOCKS / items), max(1, math.ceil(max_ctx / 256)))
+        return 1
+
     def attention(self, q, cache_k, cache_v, meta):
         n_kv, hd = cache_k.shape[1], cache_k.shape[3]
         nh = q.shape[1] // hd
         if meta.is_decode:
-            B = meta.num_seqs
-            splits = 1
-            if B * n_kv < self.TARGET_BLOCKS:
-                splits = min(math.ceil(self.TARGET_BLOCKS / (B * n_kv)), max(1, math.ceil(meta.max_ctx / 256)))
+            splits = self.decode_attn_splits(meta.num_seqs, nh, n_kv, hd, meta.max_ctx)
             return self.C.attn_decode(q, cache_k, cache_v, meta.seq_slots, meta.token_pos, nh, splits)
         tiles = getattr(meta, "_tiles", None)
         if tiles is None:

@@ -50,7 +50,8 @@ def test_bench_json_contract(n, dp):
 
 def test_auto_microbatch_groups():
     """bench.py default groups: 2 per stage when a decode step reads more KV
-    than weights (GPT-2 XL headline), 1 per stage otherwise (Llama-3 8B)."""
+    than weights on the VALU attention kernel (GPT-2 XL headline), 1 per
+    stage otherwise (Llama-3 8B: grouped-query attention on MFMA)."""
     import importlib.util
     import types
 
@@ -62,4 +63,5 @@ def test_auto_microbatch_groups():
     assert b.auto_groups(a("gpt2-xl", 512), 8) == 16
     assert b.auto_groups(a("gpt2-xl", 1), 1) == 1
     assert b.auto_groups(a("llama-3-8b", 256), 1) == 1
-    assert b.auto_groups(a("llama-3-8b", 256), 4) == 8  # 1024 sequences per stage: KV-bound again
+    assert b.auto_groups(a("llama-3-8b", 256), 4) == 4  # KV-bound, but MFMA attention is at roofline
+    assert b.auto_groups(types.SimpleNamespace(model="llama-3-8b", batch=32, prompt=4096, gen=128), 1) == 1

@@ -355,6 +355,41 @@ def test_attention_decode_mfma_grouped(C, nh, n_kv, B):
     close(o, o_valu, 2e-2)
 
 
+@pytest.mark.parametrize("splits", [2, 5, 16])
+def test_attention_decode_mfma_context_splits(C, splits):
+    """The MFMA decode kernel over context splits (long contexts, few
+    sequences): per-split partials merged by the combine kernel, including
+    splits past a short sequence's end (empty ranges) and split boundaries
+    that are not 32-key aligned."""
+    B, nh, n_kv, hd, S = 6, 32, 8, 128, 1100
+    kc, vc = bf(B + 2, n_kv, S, hd, seed=36), bf(B + 2, n_kv, S, hd, seed=37)
+    q = bf(B, nh * hd, seed=38)
+    seq_slots = torch.tensor([7, 0, 3, 5, 1, 2], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([1099, 0, 7, 517, 1023, 64], dtype=torch.int32, device=DEV)
+    cu = torch.arange(B + 1, dtype=torch.int32)
+    o_ref = ref.attention(q.reshape(B, nh, hd).cpu(), kc.cpu(), vc.cpu(), seq_slots.cpu(), pos.cpu(), cu)
+    C.attn_set_mfma_min(1)
+    try:
+        o = C.attn_decode(q, kc, vc, seq_slots, pos, nh, splits)
+    finally:
+        C.attn_set_mfma_min(256)
+    assert torch.isfinite(o.float()).all()
+    close(o.reshape(B, nh, hd), o_ref, 2e-2)
+
+
+def test_decode_attn_split_policy():
+    """Long contexts with few sequences take the MFMA kernel with context
+    splits; the headline batches stay unsplit."""
+    from llm_sharding_demo_amd.ops.hip import HipBackend as H
+
+    assert H.decode_attn_splits(256, 32, 8, 128, 400) == 1  # 2048 items
+    assert H.decode_attn_splits(32, 32, 8, 128, 4224) == 4  # 256 items -> 1024 waves
+    assert H.decode_attn_splits(8, 32, 8, 128, 8128) == 16  # 64 items -> 1024 waves
+    assert H.decode_attn_splits(4, 32, 8, 128, 8128) == 16  # >= 512 keys per split
+    assert H.decode_attn_splits(1, 32, 8, 128, 300) == 2  # VALU split rule
+    assert H.decode_attn_splits(64, 25, 25, 64, 300) == 1  # GPT-2 XL: VALU
+
+
 @pytest.mark.parametrize("hd,nh,n_kv", [(64, 4, 4), (128, 8, 2)])
 def test_attention_prefill_ragged_chunked(C, hd, nh, n_kv):
     from llm_sharding_demo_amd.ops.hip import prefill_tiles

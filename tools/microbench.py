@@ -226,7 +226,7 @@ def bench_resid_norm(M, N, K, splits_list, label=""):
             report(f"resid+norm{label} M={M} N={N} K={K} S={S} defer={int(defer)}", us, N * K * 2)
 
 
-def bench_attn_decode(B, nh, n_kv, hd, ctx, slots=None):
+def bench_attn_decode(B, nh, n_kv, hd, ctx, slots=None, splits=None):
     slots = slots or B
     S = ctx + 1
     kc = torch.randn(slots, n_kv, S, hd, device=DEV).bfloat16()
@@ -234,7 +234,8 @@ def bench_attn_decode(B, nh, n_kv, hd, ctx, slots=None):
     q = torch.randn(B, nh * hd, device=DEV).bfloat16()
     ss = torch.arange(B, dtype=torch.int32, device=DEV)
     pos = torch.full((B,), ctx - 1, dtype=torch.int32, device=DEV)
-    splits = 1 if B * n_kv >= 512 else min(math.ceil(512 / (B * n_kv)), max(1, math.ceil(ctx / 256)))
+    if splits is None:
+        splits = 1 if B * n_kv >= 512 else min(math.ceil(512 / (B * n_kv)), max(1, math.ceil(ctx / 256)))
     us = timeit(lambda: C.attn_decode(q, kc, vc, ss, pos, nh, splits))
     report(f"attn_decode B={B} nh={nh} kv={n_kv} hd={hd} ctx={ctx} splits={splits}", us,
            B * n_kv * ctx * hd * 2 * 2)
@@ -659,6 +660,21 @@ def main():
                 print("mfma_min", mm, flush=True)
                 bench_attn_decode(B, 32, 8, 128, ctx)
         C.attn_set_mfma_min(256)
+    if "attnlong" in which:  # long-context grouped-query decode: split MFMA vs VALU
+        from llm_sharding_demo_amd.ops.hip import HipBackend
+        for B, ctx in ((32, 4224), (8, 8128), (16, 4096), (64, 2048), (32, 320), (4, 8128), (1, 8128)):
+            pol = HipBackend.decode_attn_splits(B, 32, 8, 128, ctx)
+            print("policy splits", pol, flush=True)
+            bench_attn_decode(B, 32, 8, 128, ctx, splits=pol)
+            C.attn_set_mfma_min(1 << 30)
+            print("VALU (old policy)", flush=True)
+            bench_attn_decode(B, 32, 8, 128, ctx)
+            C.attn_set_mfma_min(1)
+            for sp in (2, 4, 8, 16, 32):
+                if sp != pol and B * 8 * sp <= 8192 and ctx // sp >= 128:
+                    print("mfma splits", sp, flush=True)
+                    bench_attn_decode(B, 32, 8, 128, ctx, splits=sp)
+            C.attn_set_mfma_min(256)
     if "attnw" in which:  # full-batch decode attention: 4 vs 8 waves per block
         for hd, nh, nkv in ((128, 32, 8), (64, 25, 25)):
             for B, ctx in ((256, 160), (256, 192), (128, 192), (512, 192)):

@@ -1,10 +1,12 @@
 """One prefill-shaped GEMM per large-GEMM kernel kind, a few launches each
 (a short program for rocprofv3 --pmc passes).  usage: pmc_bigemm.py [N K]"""
+import os
 import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
 
-from llm_sharding_demo_amd.ops.hip import _load
+from llm_sharding_demo_amd.ops.hip import _load  # noqa: E402
 
 C = _load()
 N, K = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (6400, 1600)
