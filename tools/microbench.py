@@ -226,6 +226,12 @@ def bench_resid_norm(M, N, K, splits_list, label=""):
             report(f"resid+norm{label} M={M} N={N} K={K} S={S} defer={int(defer)}", us, N * K * 2)
 
 
+def HipBackendSplits(*a):
+    from llm_sharding_demo_amd.ops.hip import HipBackend
+
+    return HipBackend.decode_attn_splits(*a)
+
+
 def bench_attn_decode(B, nh, n_kv, hd, ctx, slots=None, splits=None):
     slots = slots or B
     S = ctx + 1
@@ -674,6 +680,20 @@ def main():
                 if sp != pol and B * 8 * sp <= 8192 and ctx // sp >= 128:
                     print("mfma splits", sp, flush=True)
                     bench_attn_decode(B, 32, 8, 128, ctx, splits=sp)
+            C.attn_set_mfma_min(256)
+    if "attnss" in which:  # single-stream grouped-query decode: VALU vs MFMA over context splits
+        for ctx in (192, 320, 1024):
+            C.attn_set_mfma_min(1 << 30)
+            print("VALU (policy splits)", flush=True)
+            bench_attn_decode(1, 32, 8, 128, ctx, splits=HipBackendSplits(1, 32, 8, 128, ctx))
+            for sp in (2, 4):
+                print("VALU splits", sp, flush=True)
+                bench_attn_decode(1, 32, 8, 128, ctx, splits=sp)
+            C.attn_set_mfma_min(1)
+            for sp in (1, 2, 4, 6, 8, 16):
+                if ctx // sp >= 16:
+                    print("mfma splits", sp, flush=True)
+                    bench_attn_decode(1, 32, 8, 128, ctx, splits=sp)
             C.attn_set_mfma_min(256)
     if "attnw" in which:  # full-batch decode attention: 4 vs 8 waves per block
         for hd, nh, nkv in ((128, 32, 8), (64, 25, 25)):
