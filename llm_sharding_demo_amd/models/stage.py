@@ -17,7 +17,7 @@ to P stages with an arbitrary layer range each.  Differences by design:
 """
 from __future__ import annotations
 
-from typing import Dict, Optional, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 
@@ -33,7 +33,8 @@ class StageModel:
                  last: bool, device="cpu", dtype: Optional[torch.dtype] = None, seed: int = 0,
                  weights_path: Optional[str] = None, max_slots: int = 8, max_seq: int = 1024,
                  weights: Optional[Dict[str, torch.Tensor]] = None,
-                 units: Optional[Tuple[int, int]] = None, backend=None):
+                 units: Optional[Tuple[int, int]] = None, backend=None,
+                 variants: Optional[Sequence[Tuple[int, int]]] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         if dtype is None:
@@ -45,6 +46,11 @@ class StageModel:
         if not 0 <= ua <= ub <= 2 * cfg.n_layers:
             raise ValueError(f"unit range {units} outside [0, {2 * cfg.n_layers}]")
         self.unit_start, self.unit_end = ua, ub
+        # alternating splits (parallel/partition.py make_alt_unit_plans): the
+        # unit range run for even / odd microbatch groups, both inside `units`
+        self.variants = [tuple(v) for v in variants] if variants else [(ua, ub)]
+        if any(not (ua <= a <= b <= ub) for a, b in self.variants):
+            raise ValueError(f"variant ranges {self.variants} outside the stage's units {units}")
         self.layer_start, self.layer_end = ua // 2, (ub + 1) // 2  # layers touched
         self.first, self.last = first, last
         self.layers = range(self.layer_start, self.layer_end)
@@ -117,20 +123,24 @@ class StageModel:
         return self.backend.embed(ids, meta.token_pos, self.w["embed_tokens"], None)
 
     def forward(self, meta: BatchMeta, inp: torch.Tensor, all_logits: bool = False,
-                head: bool = True, head_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+                head: bool = True, head_rows: Optional[torch.Tensor] = None,
+                variant: int = 0) -> torch.Tensor:
         """inp: token ids int32 [T] (first stage) or hidden fp32 [T, H].
 
         Returns hidden fp32 [T, H] (non-last stage, or `head=False`: a
         non-final prefill chunk only fills the KV cache) or fp32 logits
         [B, vocab_padded] for the last query of each sequence (last stage;
         [T, vocab_padded] with all_logits; the rows `head_rows` of the packed
-        batch when given -- e.g. only the prompts whose final chunk this is)."""
+        batch when given -- e.g. only the prompts whose final chunk this is).
+        `variant`: which of the stage's unit ranges to run (the microbatch
+        group's parity under alternating splits; 0 otherwise)."""
         x = self.embed(inp, meta) if self.first else inp
         r = Residual(x)
         gpt2 = self.cfg.arch == "gpt2"
         attn_fn = self._gpt2_attn if gpt2 else self._llama_attn
         mlp_fn = self._gpt2_mlp if gpt2 else self._llama_mlp
-        for u in range(self.unit_start, self.unit_end):
+        ua, ub = self.variants[variant % len(self.variants)]
+        for u in range(ua, ub):
             i = u >> 1
             if u & 1:
                 mlp_fn(i, r)

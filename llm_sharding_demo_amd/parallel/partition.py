@@ -249,6 +249,84 @@ def _native_or_python_dp(costs, P, head, first) -> UnitPlan:
     return _minmax_dp(costs, P, head)
 
 
+# ---------------------------------------------------------------------------
+# Alternating splits: two unit plans, one per microbatch-group parity
+# ---------------------------------------------------------------------------
+# Half-layer units are still coarse against a stage's share: GPT-2 XL on 8
+# stages (attention half ~83 us, MLP half ~37 us at 256 rows, ~738 us per
+# stage) leaves one stage with 7 attention halves, 91 % of an even split.
+# Groups of even index run plan A, odd groups plan B; at every boundary the
+# two plans cut at most one unit apart, so a stage's work per decode step (the
+# sum over its groups) is the MEAN of its two ranges -- quarter-layer
+# granularity on average with the same wire protocol (only the fp32 residual
+# crosses a boundary).  A stage holds the weights and KV layers of the union
+# of its two ranges (at most one extra half-layer per side); a sequence never
+# changes group, so each variant's KV cache stays on one stage.
+def _alt_dp(costs: Sequence[float], P: int, head: float) -> Tuple[UnitPlan, UnitPlan]:
+    """Min-max over the mean of two contiguous partitions.  Position p in
+    [0, 2n] cuts plan A at unit p // 2 and plan B at (p + 1) // 2; a stage
+    spans positions p1 -> p2 >= p1 + 2 (non-empty in both plans)."""
+    n = len(costs)
+    if not 1 <= P <= n:
+        raise ValueError(f"cannot split {n} units into {P} non-empty stages")
+    pre = [0.0]
+    for c in costs:
+        pre.append(pre[-1] + c)
+
+    def seg(p1: int, p2: int) -> float:
+        return 0.5 * ((pre[p2 // 2] - pre[p1 // 2]) + (pre[(p2 + 1) // 2] - pre[(p1 + 1) // 2]))
+
+    N2 = 2 * n
+    INF = float("inf")
+    best = [[INF] * (N2 + 1) for _ in range(P + 1)]
+    arg = [[0] * (N2 + 1) for _ in range(P + 1)]
+    best[0][0] = 0.0
+    for k in range(1, P + 1):
+        lo, hi = 2 * k, N2 - 2 * (P - k)
+        for p2 in (range(lo, hi + 1) if k < P else [N2]):
+            for p1 in range(2 * (k - 1), p2 - 1):
+                if best[k - 1][p1] == INF:
+                    continue
+                v = max(best[k - 1][p1], seg(p1, p2) + (head if k == P else 0.0))
+                if v < best[k][p2]:
+                    best[k][p2], arg[k][p2] = v, p1
+    cuts = [N2]
+    for k in range(P, 0, -1):
+        cuts.append(arg[k][cuts[-1]])
+    cuts.reverse()
+    plan_a = [(cuts[k] // 2, cuts[k + 1] // 2) for k in range(P)]
+    plan_b = [((cuts[k] + 1) // 2, (cuts[k + 1] + 1) // 2) for k in range(P)]
+    return plan_a, plan_b
+
+
+def make_alt_unit_plans(cfg: ModelConfig, num_stages: int, rows: int = 128,
+                        avg_ctx: int = 192) -> Tuple[UnitPlan, UnitPlan]:
+    """(plan A, plan B) for even / odd microbatch groups (see _alt_dp)."""
+    P = num_stages
+    if P == 1:
+        return [(0, 2 * cfg.n_layers)], [(0, 2 * cfg.n_layers)]
+    costs, head, embed = unit_costs(cfg, max(1, min(rows, 256)), avg_ctx)
+    costs = list(costs)
+    costs[0] += embed
+    plan_a, plan_b = _alt_dp(costs, P, head)
+    for pl in (plan_a, plan_b):
+        validate_unit_plan(pl, cfg.n_layers)
+    return plan_a, plan_b
+
+
+def alt_stage_costs(cfg: ModelConfig, plans: Tuple[UnitPlan, UnitPlan], rows: int = 128,
+                    avg_ctx: int = 192) -> List[float]:
+    """Mean per-stage cost of the two plans (what a decode step pays)."""
+    a = unit_stage_costs(cfg, plans[0], rows, avg_ctx)
+    b = unit_stage_costs(cfg, plans[1], rows, avg_ctx)
+    return [(x + y) / 2 for x, y in zip(a, b)]
+
+
+def union_plan(plans: Tuple[UnitPlan, UnitPlan]) -> UnitPlan:
+    """Per stage, the units either plan runs there (weights, KV layers)."""
+    return [(min(a0, a1), max(b0, b1)) for (a0, b0), (a1, b1) in zip(*plans)]
+
+
 def units_to_layers(plan: UnitPlan) -> Plan:
     """Layers each stage touches (a layer cut in half appears in both stages)."""
     return [(a // 2, (b + 1) // 2) for a, b in plan]

@@ -517,13 +517,14 @@ class StageWorker:
         if self.first:
             inp = _h2d([t for c in ch for t in c.ids], torch.int32, dev).to(dev, non_blocking=True)
         finals = [i for i, c in enumerate(ch) if c.final]
+        v = gp.g & 1  # alternating-split variant of this group
         if not self.last:
-            return st.forward(meta, inp, head=False)
+            return st.forward(meta, inp, head=False, variant=v)
         if not finals:
-            st.forward(meta, inp, head=False)  # KV cache only
+            st.forward(meta, inp, head=False, variant=v)  # KV cache only
             return None
         rows = meta.last_idx.index_select(0, torch.tensor(finals, dtype=torch.long, device=dev))
-        logits = st.forward(meta, inp, head=True, head_rows=rows)
+        logits = st.forward(meta, inp, head=True, head_rows=rows, variant=v)
         fc = [ch[i] for i in finals]
         samp = SamplingState([c.temperature for c in fc], [c.top_k for c in fc],
                              [c.greedy for c in fc], [c.seed for c in fc], dev)
@@ -534,7 +535,7 @@ class StageWorker:
 
         def body():
             meta = gs.meta(gp.b, gp.ctxb)
-            out = self.stage.forward(meta, inp, head=True)
+            out = self.stage.forward(meta, inp, head=True, variant=gp.g & 1)
             meta.advance()
             if not self.last:
                 return out

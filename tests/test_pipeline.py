@@ -309,3 +309,44 @@ def test_stage_busy_stats_local_and_gloo():
     st = eng.last_session.stages
     assert [s["stage"] for s in st] == [0, 1, 2]
     assert all(0.0 < s["busy_fraction"] <= 1.0 and s["items"] > 0 for s in st)
+
+
+def test_alternating_split_plans():
+    """Plans A / B (even / odd microbatch groups) cut at most one unit apart,
+    each is a valid partition, the stage union holds both, and the mean
+    per-stage cost beats the single half-layer plan (GPT-2 XL, 256 rows)."""
+    from llm_sharding_demo_amd.parallel.partition import (alt_stage_costs, make_alt_unit_plans,
+                                                          make_unit_plan, union_plan,
+                                                          unit_stage_costs, validate_unit_plan)
+
+    mc = get_model_config("gpt2-xl")
+    for P in (2, 4, 8):
+        pa, pb = make_alt_unit_plans(mc, P, rows=256)
+        for pl in (pa, pb):
+            validate_unit_plan(pl, mc.n_layers)
+        assert all(abs(a[1] - b[1]) <= 1 for a, b in zip(pa, pb))
+        un = union_plan((pa, pb))
+        assert all(u[0] <= min(a[0], b[0]) and max(a[1], b[1]) <= u[1] for u, a, b in zip(un, pa, pb))
+        alt = max(alt_stage_costs(mc, (pa, pb), rows=256))
+        one = max(unit_stage_costs(mc, make_unit_plan(mc, P, rows=256), rows=256))
+        assert alt <= one + 1e-6
+    pa, pb = make_alt_unit_plans(mc, 8, rows=256)
+    costs = alt_stage_costs(mc, (pa, pb), rows=256)
+    assert sum(costs) / 8 / max(costs) > 0.95  # half-layer units alone: ~0.92
+
+
+@pytest.mark.parametrize("P,M", [(2, 2), (3, 6), (4, 4)])
+def test_alternating_split_matches_unsplit(golden, P, M):
+    """Even / odd groups on different unit ranges: tokens equal the unsplit
+    model; the compat full-sequence path (variant 0) still chains correctly."""
+    cfg = EngineConfig(model_id="gpt2-test", num_stages=P, max_batch=8, device="cpu",
+                       num_microbatches=M)
+    eng = Engine(cfg)
+    assert eng.unit_plans is not None and eng.unit_plans[0] != eng.unit_plans[1]
+    out = eng.generate_ids(PROMPTS, SamplingParams(greedy=True, max_new_tokens=6))
+    assert out == golden
+    ref = Engine(EngineConfig(model_id="gpt2-test", num_stages=2, max_batch=8, device="cpu",
+                              num_microbatches=1))  # odd group count: one plan
+    assert ref.unit_plans is None
+    torch.testing.assert_close(eng.forward_b(eng.forward_a([5, 6, 7, 8])),
+                               ref.forward_b(ref.forward_a([5, 6, 7, 8])), atol=1e-4, rtol=1e-4)
