@@ -53,6 +53,10 @@ def parse():
     p.add_argument("--loopback-stages", type=int, default=0,
                    help="rehearsal: run this many pipeline stages as threads on ONE GPU "
                         "(device-async loopback transport); --batch is then the total batch")
+    p.add_argument("--prefill-chunk", type=int, default=int(os.environ.get("BENCH_PREFILL_CHUNK", "0")),
+                   help="prompt tokens per prefill chunk (0: whole prompts).  Chunks shorten the pipeline "
+                        "fill at P >= 2 stages; measured free on one stage but +1.5 %% per step in the 8-stage "
+                        "loopback rehearsal (profiles/r2_prefill_chunk.log), so off by default")
     p.add_argument("--device", default="cuda",
                    help="cuda (MI355X); cpu only to rehearse the multi-rank contract with gloo")
     p.add_argument("--greedy", action="store_true")
@@ -109,7 +113,9 @@ def main() -> int:
         P = args.loopback_stages
         M = args.microbatches or auto_groups(args, P)
         transport = "loopback"
+    chunk = max(0, args.prefill_chunk)
     cfg = EngineConfig(model_id=args.model, num_stages=P, dp_replicas=R, max_batch=Br,
+                       prefill_chunk=chunk,
                        max_seq_len=args.prompt + args.gen, device=args.device,
                        use_graphs=not args.no_graphs, num_microbatches=M, seed=args.seed,
                        transport=transport)
@@ -183,6 +189,7 @@ def main() -> int:
             "max_decode_step_ms": round(statistics.mean(max_step), 3) if max_step else None,
             "config": {"model": args.model, "global_batch": B, "seq_len": args.prompt + args.gen,
                        "prompt_len": args.prompt, "gen_tokens": args.gen, "microbatches": M,
+                       "prefill_chunk": chunk,
                        "parallelism": f"pp{P}" + (f"xdp{R}" if R > 1 else "")
                        + ("-loopback-1gpu" if args.loopback_stages else ""),
                        "sampler": "greedy" if args.greedy else "T0.6/top-k40",
