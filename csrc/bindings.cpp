@@ -25,6 +25,7 @@ void lsd_gemm_set_tiled3_max(int v);
 void lsd_gemm_set_ring_slots(int v);
 void lsd_gemm_set_ring_tn(int v);
 void lsd_gemm_set_ring_fill(int v);
+void lsd_gemm_set_ring_m96(int v);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
 void lsd_attn_set_large_waves(int hd, int v);
@@ -534,6 +535,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_ring_slots", [](int64_t v) { lsd_gemm_set_ring_slots((int)v); });
   m.def("gemm_set_ring_tn", [](int64_t v) { lsd_gemm_set_ring_tn((int)v); });
   m.def("gemm_set_ring_fill", [](int64_t v) { lsd_gemm_set_ring_fill((int)v); });
+  m.def("gemm_set_ring_m96", [](int64_t v) { lsd_gemm_set_ring_m96((int)v); });
   // decode attention: cap the grid (blocks loop over (sequence, head) items)
   m.def("attn_set_max_wg", [](int64_t v) { lsd_attn_set_max_wg((int)v); });
   // decode attention: waves per block when the batch has few (sequence, head) items

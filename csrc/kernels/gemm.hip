@@ -538,22 +538,23 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk)
 // into a 16-byte row-contiguous vector (256 B per 16 lanes).
 // TN = tile columns (128, or 64 for the narrow ring tiles); wave (wm, wn)
 // holds rows wm*64 + [0, 64) and columns wn*TN/2 + [0, TN/2).
-template <int EPI, int TN = TBN>
-__device__ __forceinline__ void tiled_epilogue(const GemmParams& p, f32x4 (&acc)[4][TN / 32], char* smem,
+template <int EPI, int TN = TBN, int MI = 4>
+__device__ __forceinline__ void tiled_epilogue(const GemmParams& p, f32x4 (&acc)[MI][TN / 32], char* smem,
                                                int m0, int n0, int split, int wm, int wn, int r,
                                                int g) {
   constexpr int CLD = TN + 4;  // bank skew
   constexpr int CPR = TN / 8;  // 8-column chunks per row
+  constexpr int TM = 32 * MI;  // tile rows (wave rows of 16 * MI)
   float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < TN / 32; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        ct[(wm * 64 + i * 16 + 4 * g + q) * CLD + wn * (TN / 2) + j * 16 + r] = acc[i][j][q];
+        ct[(wm * 16 * MI + i * 16 + 4 * g + q) * CLD + wn * (TN / 2) + j * 16 + r] = acc[i][j][q];
   __syncthreads();
-  for (int c = threadIdx.x; c < TBM * CPR; c += 256) {
+  for (int c = threadIdx.x; c < TM * CPR; c += 256) {
     const int row = c / CPR, n = n0 + (c % CPR) * 8, m = m0 + row;
     if (m >= p.M || n >= p.N) continue;
     const float* src = ct + row * CLD + (c % CPR) * 8;
@@ -647,29 +648,33 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(GemmParams p, int tiles
 // (tools/microbench.py tiled3, GPT-2 XL): QKV 25.8 (double buffer) -> 20.5
 // (ring, 128 x 128) -> 15.6 us (ring, 128 x 64); MLP-up 29.4 -> 23.5 -> 17.3 us;
 // split-K decode kernel 23.3 / 26.2 us, hipBLASLt 19.3 / 20.0 us.
-template <int SLOTS, int TN>
+template <int SLOTS, int TN, int TM = TBM>
 constexpr int smem_ring() {
-  return TBM * (TN + 4) * 4 > SLOTS * (TILE_BYTES + TN * TBK * 2) ? TBM * (TN + 4) * 4
-                                                                 : SLOTS * (TILE_BYTES + TN * TBK * 2);
+  return TM * (TN + 4) * 4 > SLOTS * (TM + TN) * TBK * 2 ? TM * (TN + 4) * 4 : SLOTS * (TM + TN) * TBK * 2;
 }
 
 // s_waitcnt immediate for vmcnt(n) alone (gfx9 layout: vmcnt[3:0] | vmcnt[5:4] << 14)
 constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
 
-template <int EPI, int SLOTS, int TN>
+// MI = 16-row MFMA tiles per wave: 4 (128-row tiles) or 3 (96-row tiles: a
+// 256-row decode GEMM as 3 row tiles -- 3/4 of the A bytes per workgroup
+// where 3 x the column tiles still fit the chip in one round).
+template <int EPI, int SLOTS, int TN, int MI = 4>
 __global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int D = SLOTS - 1;                    // prefetch distance (k-steps in flight)
   constexpr int JT = TN / 32;                     // 16-column MFMA tiles per wave
-  constexpr int SLOT_BYTES = TILE_BYTES + TN * TBK * 2;
-  constexpr int LPS = 4 + TN / 32;                // glds per thread per k-step (A + W)
-  __shared__ __attribute__((aligned(16))) char smem[smem_ring<SLOTS, TN>()];  // [slot][A|W]; then C tile
+  constexpr int TM = 32 * MI;                     // tile rows
+  constexpr int A_BYTES = TM * TBK * 2;
+  constexpr int SLOT_BYTES = A_BYTES + TN * TBK * 2;
+  constexpr int LPS = MI + TN / 32;               // glds per thread per k-step (A + W)
+  __shared__ __attribute__((aligned(16))) char smem[smem_ring<SLOTS, TN, TM>()];  // [slot][A|W]; then C tile
   const int nwg = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int per_split = tiles_m * tiles_n;
   const int split = bid / per_split;
   const int t = bid % per_split;
   const int tm = t % tiles_m, tn = t / tiles_m;
-  const int m0 = tm * TBM, n0 = tn * TN;
+  const int m0 = tm * TM, n0 = tn * TN;
   const int KT = p.K / TBK;
   const int kb = (int)((long)KT * split / p.splits), ke = (int)((long)KT * (split + 1) / p.splits);
 
@@ -677,16 +682,16 @@ __global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_
   const int wm = w >> 1, wn = w & 1;
   const int r = lane & 15, g = lane >> 4;
 
-  f32x4 acc[4][JT];
+  f32x4 acc[MI][JT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto issue = [&](int kt, int slot) {
     char* b = smem + slot * SLOT_BYTES;
-    stage_tile<TBM>(b, p.A, p.lda, m0, p.M - 1, kt * TBK);
-    stage_tile<TN>(b + TILE_BYTES, p.W, p.ldw, n0, p.N - 1, kt * TBK);
+    stage_tile<TM>(b, p.A, p.lda, m0, p.M - 1, kt * TBK);
+    stage_tile<TN>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, kt * TBK);
   };
   static_assert(SLOTS == 3 || SLOTS == 4, "ring of 3 or 4 slots");
   static_assert(2 * LPS <= 63, "vmcnt holds at most 63 outstanding loads");
@@ -702,23 +707,23 @@ __global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_
     __builtin_amdgcn_s_barrier();
     if (kt + D < ke) issue(kt + D, slot == 0 ? SLOTS - 1 : slot - 1);
     const char* ta = smem + slot * SLOT_BYTES;
-    const char* tw = ta + TILE_BYTES;
+    const char* tw = ta + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], wf[JT];
+      bf16x8 af[MI], wf[JT];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = lds_frag(ta, wm * 64 + i * 16 + r, kk * 4 + g);
+      for (int i = 0; i < MI; ++i) af[i] = lds_frag(ta, wm * 16 * MI + i * 16 + r, kk * 4 + g);
 #pragma unroll
       for (int j = 0; j < JT; ++j) wf[j] = lds_frag(tw, wn * (TN / 2) + j * 16 + r, kk * 4 + g);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < JT; ++j) acc[i][j] = mfma16(af[i], wf[j], acc[i][j]);
     }
     slot = slot == SLOTS - 1 ? 0 : slot + 1;
   }
   __syncthreads();  // every wave's fragment reads retired before the C tile overwrites the slots
-  tiled_epilogue<EPI, TN>(p, acc, smem, m0, n0, split, wm, wn, r, g);
+  tiled_epilogue<EPI, TN, MI>(p, acc, smem, m0, n0, split, wm, wn, r, g);
 }
 
 // ---------------------------------------------------------------------------
@@ -1195,6 +1200,7 @@ static int g_tiled3_max_blocks = 0;
 static int g_ring_slots = 3;  // lsd_gemm_set_ring_slots(): 3 or 4
 static int g_ring_tn = 128;   // lsd_gemm_set_ring_tn(): ring tile columns, 128, 64, 32 or 0 (auto 32/64)
 static int g_ring_fill = 128; // auto: 32-wide tiles below this many 64-wide workgroups
+static int g_ring_m96 = 0;    // lsd_gemm_set_ring_m96(): largest 96-row-tile ring grid (0 = off)
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
 // with N = H), M > g_sk_rows rows run as ceil(M / g_sk_rows) row blocks
@@ -1279,6 +1285,21 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
         return hipGetLastError();
       }
     }
+    // 96-row tiles above 128 rows while 3 x the column tiles fit one round
+    // on the chip (GPT-2 XL QKV at 256 rows: 225 workgroups of 512 KB of
+    // operand traffic instead of 150 of 614 KB; the ring GEMMs are bound by
+    // L2 -> CU bytes per workgroup, profiles/r2_decode_gemm_limits.log).
+    // Alone 10-12 % faster (QKV 16.3 -> 14.7 us at 256 rows, MLP-up 17.1 ->
+    // 15.0 at 192), but beside the other microbatch lane the extra
+    // workgroups cost more than they save (bench: 384 sequences -1 to -1.4 %,
+    // 512 within +-0.5 %; profiles/r2_ring_m96.log) -- off by default.
+    if (p.splits == 1 && p.M > TBM && g_ring_m96 > 0) {
+      const int tm96 = (p.M + 95) / 96;
+      if (tm96 * tn64 <= g_ring_m96) {
+        hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 64, 3>), dim3(tm96 * tn64), dim3(256), 0, st, p, tm96, tn64);
+        return hipGetLastError();
+      }
+    }
     if (tm * tn64 * p.splits <= g_tiled3_max_blocks) {
       hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 64>), dim3(tm * tn64 * p.splits), dim3(256), 0, st, p, tm, tn64);
       return hipGetLastError();
@@ -1310,6 +1331,7 @@ extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }
 extern "C" void lsd_gemm_set_ring_fill(int v) { g_ring_fill = v; }
+extern "C" void lsd_gemm_set_ring_m96(int v) { g_ring_m96 = v; }
 extern "C" int lsd_gemm_sk_rblocks(int M, int N, int S) { return sk_rblocks(M, N, S); }
 extern "C" int lsd_gemm_sk_rows(int M, int N, int S) {  // rows per row block
   return sk_mt(M, sk_rblocks(M, N, S)) * 16;

@@ -158,6 +158,10 @@ class HipBackend(Backend):
     # 17.2 -> 14.2; at 256 rows the 64-wide tiles stay faster (15.6 vs 18.6)
     # (profiles/r2_ring_tn32.log)
     RING_FILL = int(os.environ.get("LSD_RING_FILL", "128"))
+    # above 128 rows: 96-row ring tiles when 3 x the 64-wide column tiles are at
+    # most this many workgroups (0 = off, default: faster alone, slower beside
+    # the other lane; gemm.hip, profiles/r2_ring_m96.log); unsplit GEMMs only
+    RING_M96 = int(os.environ.get("LSD_RING_M96", "0"))
     # Decode GEMMs leave split-K for the tiled kernels (the 128x64 LDS ring at
     # these grid sizes) above TILED_ALL_M rows at any width, and above
     # TILED_MIN_M rows when at least TILED_MIN_N wide.  bench tok/s (1 MI355X,
@@ -180,6 +184,7 @@ class HipBackend(Backend):
         self.C.gemm_set_ring_slots(self.RING_SLOTS)
         self.C.gemm_set_ring_tn(self.RING_TN)
         self.C.gemm_set_ring_fill(self.RING_FILL)
+        self.C.gemm_set_ring_m96(self.RING_M96)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))

@@ -205,6 +205,36 @@ def test_ring_gemm_epilogues(RING, CNT, M, K):
         close(x, x_ref, 2e-3, 1e-3)
 
 
+@pytest.mark.parametrize("M", [129, 200, 256, 300])
+@pytest.mark.parametrize("K", [64, 192, 640])
+def test_ring_gemm_96_row_tiles(C, CNT, M, K):
+    """Ring kernel with 96-row tiles (3 MFMA row tiles per wave): every
+    epilogue, partial row / column tiles, k-steps fewer than and beyond the ring."""
+    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
+
+    C.gemm_set_tiled3_max(1 << 30)
+    C.gemm_set_ring_tn(64)
+    C.gemm_set_ring_m96(1 << 30)
+    try:
+        N = 352
+        a, w, bias = bf(M, K, seed=66), bf(N, K, scale=0.05, seed=67), bf(N, scale=0.1, seed=68)
+        y_ref = ref.linear(a, w, bias)
+        close(C.linear(a, w, bias, 0, True, 1, CNT), y_ref, 3e-2)
+        close(C.linear(a, w, bias, 1, True, 1, CNT), ref.gelu_new(y_ref), 3e-2)
+        w2 = w[:256].contiguous()
+        y = C.linear(a, interleave_gate_up(w2, 128).contiguous(), None, 2, True, 1, CNT)
+        close(y, ref.silu_mul(*ref.linear(a, w2).split(128, 1)), 3e-2)
+        close(C.linear_f32(a, w, True, 1, CNT), ref.linear(a, w), 2e-3, 1e-3)
+        x = torch.randn(M, N, device=DEV)
+        x_ref = x + y_ref
+        assert C.linear_residual(a, w, bias, x, 1, True, CNT, False) is None
+        close(x, x_ref, 2e-3, 1e-3)
+    finally:
+        C.gemm_set_ring_m96(0)
+        C.gemm_set_tiled3_max(0)
+        C.gemm_set_ring_tn(128)
+
+
 @pytest.fixture
 def BIG(C):
     """Force the pipelined 256x256 kernel for every tiled launch with M >= 256."""
