@@ -53,10 +53,12 @@ def parse():
     p.add_argument("--loopback-stages", type=int, default=0,
                    help="rehearsal: run this many pipeline stages as threads on ONE GPU "
                         "(device-async loopback transport); --batch is then the total batch")
-    p.add_argument("--prefill-chunk", type=int, default=int(os.environ.get("BENCH_PREFILL_CHUNK", "0")),
-                   help="prompt tokens per prefill chunk (0: whole prompts).  Chunks shorten the pipeline "
-                        "fill at P >= 2 stages; measured free on one stage but +1.5 %% per step in the 8-stage "
-                        "loopback rehearsal (profiles/r2_prefill_chunk.log), so off by default")
+    p.add_argument("--prefill-chunk", type=int, default=int(os.environ.get("BENCH_PREFILL_CHUNK", "-1")),
+                   help="prompt tokens per prefill chunk (0: whole prompts); -1 -> auto: whole prompts on "
+                        "one stage, prompt/4 (>= 32) on P >= 2 stages.  Chunks shorten the pipeline fill "
+                        "(the last stage idles (P-1) x one group's prefill time per session) and cost "
+                        "nothing measurable on one stage or in the 2/4-stage loopback rehearsal "
+                        "(profiles/r2_prefill_chunk.log)")
     p.add_argument("--device", default="cuda",
                    help="cuda (MI355X); cpu only to rehearse the multi-rank contract with gloo")
     p.add_argument("--greedy", action="store_true")
@@ -113,7 +115,10 @@ def main() -> int:
         P = args.loopback_stages
         M = args.microbatches or auto_groups(args, P)
         transport = "loopback"
-    chunk = max(0, args.prefill_chunk)
+    chunk = args.prefill_chunk
+    if chunk < 0:
+        chunk = 0 if P == 1 else max(32, args.prompt // 4)
+        chunk = 0 if chunk >= args.prompt else chunk
     cfg = EngineConfig(model_id=args.model, num_stages=P, dp_replicas=R, max_batch=Br,
                        prefill_chunk=chunk,
                        max_seq_len=args.prompt + args.gen, device=args.device,
