@@ -136,10 +136,11 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,dp", [(2, 1), (3, 1), (4, 2), (2, 2)])
-def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp):
+@pytest.mark.parametrize("world,dp,chunk", [(2, 1, 0), (3, 1, 0), (4, 2, 0), (2, 2, 0), (3, 1, 2)])
+def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp, chunk):
     """One process per stage, torch.distributed gloo (the RCCL path's twin);
-    dp > 1: `dp` pipeline replicas of world/dp stages share the requests."""
+    dp > 1: `dp` pipeline replicas of world/dp stages share the requests;
+    chunk > 0: chunked prefill through a middle stage (bench.py's P >= 2 default)."""
     script = tmp_path / "w.py"
     script.write_text(textwrap.dedent(f"""
         import sys, json, torch
@@ -147,7 +148,7 @@ def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp):
         from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
         from llm_sharding_demo_amd.runtime.engine import build_engine
         cfg = EngineConfig(model_id="gpt2-test", max_batch=8, device="cpu", transport="gloo",
-                           num_microbatches=2, dp_replicas={dp})
+                           num_microbatches=2, dp_replicas={dp}, prefill_chunk={chunk})
         eng = build_engine(cfg)
         assert (eng.P, eng.R) == ({world // dp}, {dp})
         if eng.rank != 0:
