@@ -242,7 +242,10 @@ class Engine:
         st = self.stages[0]
         return {"kv_slots": self.kv_slots, "kv_bytes_stage0": st.kv.nbytes,
                 "kv_slots_free": sum(p.available for p in self.slot_pools),
-                "group_rows": self.group_cap, "groups": self.M}
+                "group_rows": self.group_cap, "groups": self.M,
+                # half-layer unit ranges per stage: one plan, or (even, odd) group plans
+                "stage_units": [list(map(list, p)) for p in self.unit_plans] if self.unit_plans
+                else [list(map(list, self.unit_plan))]}
 
     # ------------------------------------------------------------------
     # requests
