@@ -136,10 +136,12 @@ def test_graphs_cached_across_sessions():
     assert sum(w.captures for w in e.workers) == c
 
 
-@pytest.mark.parametrize("P", [2, 4])
-def test_loopback_multi_stage_bit_identical(P):
+@pytest.mark.parametrize("P,chunk", [(2, 0), (4, 0), (3, 2), (4, 1)])
+def test_loopback_multi_stage_bit_identical(P, chunk):
     """P stage threads on one GPU with the device-async loopback transport
-    (stream waits on events, no host sync) produce the P = 1 tokens."""
+    (stream waits on events, no host sync) produce the P = 1 tokens; with
+    alternating splits (2P groups) and, for chunk > 0, chunked prefill
+    through the middle stages (bench.py's multi-stage default)."""
     sp = SamplingParams(temperature=0.8, top_k=20, seed=7, max_new_tokens=10)
     prompts = [[i + 1, 2 * i + 3, 5] for i in range(12)]
     # same microbatch shapes on one stage: a 16-row group would run the
@@ -147,10 +149,11 @@ def test_loopback_multi_stage_bit_identical(P):
     # not bit-equal -- tools/check_m1.py)
     one = _engine("gpt2-test", num_microbatches=2 * P).generate_ids(prompts, sp)
     e = Engine(EngineConfig(model_id="gpt2-test", num_stages=P, max_batch=16, device="cuda",
-                            num_microbatches=2 * P, transport="loopback"))
+                            num_microbatches=2 * P, transport="loopback", prefill_chunk=chunk))
     from llm_sharding_demo_amd.parallel.comm import LoopbackTransport
 
     assert isinstance(e.workers[1].t, LoopbackTransport)
+    assert e.unit_plans is not None  # even / odd groups on different unit ranges
     assert e.generate_ids(prompts, sp) == one
     assert e.generate_ids(prompts, sp) == one  # replayed graphs
     e.shutdown()
