@@ -147,7 +147,9 @@ def test_loopback_multi_stage_bit_identical(P, chunk):
     # same microbatch shapes on one stage: a 16-row group would run the
     # split-K GEMM where 4-row groups run the GEMV (equal to bf16 rounding,
     # not bit-equal -- tools/check_m1.py)
-    one = _engine("gpt2-test", num_microbatches=2 * P).generate_ids(prompts, sp)
+    # chunked and one-shot prefill round differently (other GEMM row counts
+    # and kernels), so the one-stage reference uses the same chunks
+    one = _engine("gpt2-test", num_microbatches=2 * P, prefill_chunk=chunk).generate_ids(prompts, sp)
     e = Engine(EngineConfig(model_id="gpt2-test", num_stages=P, max_batch=16, device="cuda",
                             num_microbatches=2 * P, transport="loopback", prefill_chunk=chunk))
     from llm_sharding_demo_amd.parallel.comm import LoopbackTransport
