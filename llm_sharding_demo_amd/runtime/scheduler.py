@@ -420,6 +420,7 @@ class _Meta:
     req: Request
     seed: int
     tokens: List[int] = field(default_factory=list)
+    done: bool = False  # finished by this scheduler (plain flag: the readout loop's hot path)
 
 
 class Scheduler:
@@ -555,29 +556,40 @@ class Scheduler:
             self._assign(host, key)
 
     def _assign(self, host: torch.Tensor, key) -> None:
+        """Apply one group readout: one event per row (plain tokens are the
+        common case and take the short path -- at 16 groups x 256 rows per
+        step this loop is the largest host cost of stage 0)."""
         rep, step, g = key
         events = self.core.assign(rep, step, g, host.tolist(), self.eng.mcfg.eos_token_id)
         now = time.monotonic()
-        meta = self.meta
+        get = self.meta.get
         for sid, tok, flags in events:
+            if not flags:
+                m = get(sid)
+                if m is not None and not m.done:
+                    m.tokens.append(tok)
+                continue
             if flags & EV_RELEASE:
-                m = meta.pop(sid, None)
-                if m is not None and flags & EV_FINISH and not m.req.done:
+                m = self.meta.pop(sid, None)
+                if m is not None and flags & EV_FINISH and not m.done:
+                    m.done = True
                     m.req.finish(list(m.tokens))
                 continue
-            m = meta.get(sid)
-            if m is None or m.req.done:
+            m = get(sid)
+            if m is None or m.done:
                 continue
             if flags & EV_FIRST:
                 m.req.t_first = now
             m.tokens.append(tok)
             if flags & EV_FINISH:
+                m.done = True
                 m.req.finish(list(m.tokens))
 
     # -- failure -----------------------------------------------------------------
     def fail_all(self, err: BaseException) -> None:
         for m in self.meta.values():
             if not m.req.done:
+                m.done = True
                 m.req.finish(error=err)
         self.meta.clear()
         self.core.reset()
