@@ -1,7 +1,7 @@
 """Op backends.
 
-The model code (models/gpt2.py, models/llama.py) is written once against the
-`Backend` interface below.  Two implementations exist:
+The model code (models/stage.py: the GPT-2 and Llama blocks of one pipeline
+stage) is written once against the `Backend` interface below.  Two implementations exist:
 
 * `ReferenceBackend` -- plain PyTorch in fp32 (ops/reference.py).  Used on CPU
   (tests, golden numerics, the tiny-gpt2 reference config).
