@@ -53,7 +53,7 @@ void lsd_gemv_set_nt(int v);
 hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st);
 hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                       const int* topk, const int* greedy, const long long* seeds,
-                      const long long* step, int* out, hipStream_t st);
+                      long long* step, int* out, int advance, hipStream_t st);
 }
 
 namespace {
@@ -480,8 +480,9 @@ torch::Tensor attn_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc,
   return out;
 }
 
-torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
-                     torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step) {
+void sample_launch(const torch::Tensor& logits, int64_t V, const torch::Tensor& temp,
+                   const torch::Tensor& topk, const torch::Tensor& greedy, const torch::Tensor& seeds,
+                   torch::Tensor& step, torch::Tensor& out, bool advance) {
   need(logits, torch::kFloat32, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && V <= logits.size(1) && V >= 1, "logits [B, >=V]");
   TORCH_CHECK(logits.stride(0) % 4 == 0 && logits.size(1) % 4 == 0, "logits row length must be a multiple of 4");
@@ -494,13 +495,28 @@ torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch:
   need(step, torch::kInt64, "step");
   TORCH_CHECK(temp.numel() == B && topk.numel() == B && greedy.numel() == B && seeds.numel() == B &&
               step.numel() == B, "sampling params must be [B]");
-  auto out = torch::empty({B}, logits.options().dtype(torch::kInt32));
+  TORCH_CHECK(step.is_contiguous(), "step must be contiguous");
+  need(out, torch::kInt32, "out");
+  TORCH_CHECK(out.numel() == B && out.is_contiguous(), "out must be contiguous int32 [B]");
   check_hip(lsd_sample(logits.data_ptr<float>(), logits.stride(0), B, V, temp.data_ptr<float>(),
                        topk.data_ptr<int>(), greedy.data_ptr<int>(),
                        reinterpret_cast<const long long*>(seeds.data_ptr<int64_t>()),
-                       reinterpret_cast<const long long*>(step.data_ptr<int64_t>()),
-                       out.data_ptr<int>(), cur_stream()), "sample");
+                       reinterpret_cast<long long*>(step.data_ptr<int64_t>()),
+                       out.data_ptr<int>(), advance ? 1 : 0, cur_stream()), "sample");
+}
+
+torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
+                     torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step) {
+  auto out = torch::empty({logits.size(0)}, logits.options().dtype(torch::kInt32));
+  sample_launch(logits, V, temp, topk, greedy, seeds, step, out, false);
   return out;
+}
+
+// Decode-step form: the sampled ids go straight into `out` (the token-return
+// vector) and each row's sampler counter advances in the same kernel.
+void sample_into(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
+                 torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step, torch::Tensor out) {
+  sample_launch(logits, V, temp, topk, greedy, seeds, step, out, true);
 }
 
 }  // namespace
@@ -519,6 +535,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_decode", &attn_decode);
   m.def("attn_prefill", &attn_prefill);
   m.def("sample", &sample);
+  m.def("sample_into", &sample_into);
   m.def("gemv", &gemv);
   // GEMV weight stream with non-temporal loads (A/B knob, LSD_GEMV_NT)
   m.def("gemv_set_nt", [](int64_t v) { lsd_gemv_set_nt((int)v); });

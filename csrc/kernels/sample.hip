@@ -96,8 +96,8 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
                                                     const int* __restrict__ topk,
                                                     const int* __restrict__ greedy,
                                                     const long long* __restrict__ seeds,
-                                                    const long long* __restrict__ step,
-                                                    int* __restrict__ out) {
+                                                    long long* __restrict__ step,
+                                                    int* __restrict__ out, int advance) {
   __shared__ unsigned hist[4096];
   __shared__ float cval[SMAX];
   __shared__ int cidx[SMAX];
@@ -132,6 +132,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
       for (int w = 1; w < NT / 64; ++w)
         if (redv[w] > best || (redv[w] == best && redi[w] < bi)) { best = redv[w]; bi = redi[w]; }
       out[row] = bi;
+      if (advance) step[row] = step_r + 1;  // every thread read step[row] before the barrier above
     }
     return;
   }
@@ -373,7 +374,10 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     const int l0 = h0 ? __builtin_ctzll(h0) : 64, l1 = h1 ? __builtin_ctzll(h1) : 64;
     if (l0 < 64 || l1 < 64) pick = l0 <= l1 ? 2 * l0 : 2 * l1 + 1;
     const int win = __shfl(pick & 1 ? ix[1] : ix[0], pick >> 1, 64);
-    if (tid == 0) out[row] = win;
+    if (tid == 0) {
+      out[row] = win;
+      if (advance) step[row] = step_r + 1;
+    }
     return;
   }
   // ---- bitonic sort of the winners / candidates: (value desc, index asc); pad to pow2
@@ -425,7 +429,10 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
       if (hit) { pick = base + __builtin_ctzll(hit); break; }
       run += __shfl(pre, 63, 64);
     }
-    if (tid == 0) out[row] = cidx[pick];
+    if (tid == 0) {
+      out[row] = cidx[pick];
+      if (advance) step[row] = step_r + 1;
+    }
   }
 }
 
@@ -433,12 +440,14 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
 
 using namespace lsd;
 
+// advance != 0: also step[row] += 1 after the draw (the decode step's
+// sampler-counter advance, folded in instead of a separate add kernel)
 extern "C" hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                                  const int* topk, const int* greedy, const long long* seeds,
-                                 const long long* step, int* out, hipStream_t st) {
+                                 long long* step, int* out, int advance, hipStream_t st) {
   if (B == 0) return hipSuccess;
   if (ld % 4 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(NT), 0, st, logits, ld, V, temp, topk, greedy,
-                     seeds, step, out);
+                     seeds, step, out, advance);
   return hipGetLastError();
 }

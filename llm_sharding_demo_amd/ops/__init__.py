@@ -108,6 +108,11 @@ class ReferenceBackend(Backend):
         return ref.sample(logits, samp.temperature, samp.top_k, samp.greedy,
                           samp.uniforms(), vocab)
 
+    def sample_into(self, logits, samp, vocab: int, out) -> None:
+        """Decode step: sampled ids into `out`, then the sampler counters advance."""
+        out.copy_(self.sample(logits, samp, vocab))
+        samp.advance()
+
     def gather_rows(self, x, idx):
         return x.index_select(0, idx.long())
 

@@ -409,5 +409,10 @@ class HipBackend(Backend):
         return self.C.sample(logits, vocab, samp.temperature, samp.top_k, samp.greedy,
                              samp.seeds, samp.step)
 
+    def sample_into(self, logits, samp, vocab: int, out) -> None:
+        # one kernel: draw into `out`, advance the per-row sampler counters
+        self.C.sample_into(logits, vocab, samp.temperature, samp.top_k, samp.greedy,
+                           samp.seeds, samp.step, out)
+
     def gather_rows(self, x, idx):
         return x.index_select(0, idx.long())

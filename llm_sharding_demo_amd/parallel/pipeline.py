@@ -540,9 +540,7 @@ class StageWorker:
             if not self.last:
                 return out
             samp = gs.samp(gp.b)
-            tok = self.stage.backend.sample(out, samp, self.stage.cfg.vocab_size)
-            samp.advance()
-            gs.tokret[: gp.b].copy_(tok)
+            self.stage.backend.sample_into(out, samp, self.stage.cfg.vocab_size, gs.tokret[: gp.b])
             return gs.tokret[: gp.b]
 
         graphs = self.use_graphs and self.device.type == "cuda"

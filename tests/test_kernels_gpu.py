@@ -470,6 +470,12 @@ def test_sampler(C):
     exp = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), greedy.cpu(),
                      counter_uniform(seeds.cpu(), step.cpu()), V)
     assert out.cpu().tolist() == exp.tolist()
+    # decode-step form: same draw written into a slice, counters advanced in-kernel
+    buf = torch.full((B + 3,), -1, dtype=torch.int32, device=DEV)
+    st2 = step.clone()
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st2, buf[:B])
+    assert buf[:B].cpu().tolist() == exp.tolist() and buf[B:].cpu().tolist() == [-1] * 3
+    assert torch.equal(st2, step + 1)
     for r in range(B):
         k = 1 if greedy[r] else int(topk[r])
         assert int(out[r]) in set(torch.topk(logits[r, :V], k).indices.tolist())
@@ -501,3 +507,9 @@ def test_sampler_fast_path_and_ties(C, case):
     exp = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), greedy.cpu(),
                      counter_uniform(seeds.cpu(), step.cpu()), V)
     assert out.cpu().tolist() == exp.tolist()
+    # decode-step form: same draw written into a slice, counters advanced in-kernel
+    buf = torch.full((B + 3,), -1, dtype=torch.int32, device=DEV)
+    st2 = step.clone()
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st2, buf[:B])
+    assert buf[:B].cpu().tolist() == exp.tolist() and buf[B:].cpu().tolist() == [-1] * 3
+    assert torch.equal(st2, step + 1)
