@@ -97,7 +97,8 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
                                                     const int* __restrict__ greedy,
                                                     const long long* __restrict__ seeds,
                                                     long long* __restrict__ step,
-                                                    int* __restrict__ out, int advance) {
+                                                    int* __restrict__ out, int advance,
+                                                    const int* __restrict__ active) {
   __shared__ unsigned hist[4096];
   __shared__ float cval[SMAX];
   __shared__ int cidx[SMAX];
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
       for (int w = 1; w < NT / 64; ++w)
         if (redv[w] > best || (redv[w] == best && redi[w] < bi)) { best = redv[w]; bi = redi[w]; }
       out[row] = bi;
-      if (advance) step[row] = step_r + 1;  // every thread read step[row] before the barrier above
+      if (advance) step[row] = step_r + (active ? active[row] : 1);  // all threads read step[row] before the barrier
     }
     return;
   }
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     const int win = __shfl(pick & 1 ? ix[1] : ix[0], pick >> 1, 64);
     if (tid == 0) {
       out[row] = win;
-      if (advance) step[row] = step_r + 1;
+      if (advance) step[row] = step_r + (active ? active[row] : 1);
     }
     return;
   }
@@ -431,7 +432,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     }
     if (tid == 0) {
       out[row] = cidx[pick];
-      if (advance) step[row] = step_r + 1;
+      if (advance) step[row] = step_r + (active ? active[row] : 1);
     }
   }
 }
@@ -440,14 +441,16 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
 
 using namespace lsd;
 
-// advance != 0: also step[row] += 1 after the draw (the decode step's
-// sampler-counter advance, folded in instead of a separate add kernel)
+// advance != 0: also step[row] += active[row] (1 when active is null) after
+// the draw -- the decode step's sampler-counter advance (pad rows stay put),
+// folded in instead of a conversion copy + add kernel
 extern "C" hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                                  const int* topk, const int* greedy, const long long* seeds,
-                                 long long* step, int* out, int advance, hipStream_t st) {
+                                 long long* step, int* out, int advance, const int* active,
+                                 hipStream_t st) {
   if (B == 0) return hipSuccess;
   if (ld % 4 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(NT), 0, st, logits, ld, V, temp, topk, greedy,
-                     seeds, step, out, advance);
+                     seeds, step, out, advance, active);
   return hipGetLastError();
 }

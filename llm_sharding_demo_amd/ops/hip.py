@@ -412,7 +412,7 @@ class HipBackend(Backend):
     def sample_into(self, logits, samp, vocab: int, out) -> None:
         # one kernel: draw into `out`, advance the per-row sampler counters
         self.C.sample_into(logits, vocab, samp.temperature, samp.top_k, samp.greedy,
-                           samp.seeds, samp.step, out)
+                           samp.seeds, samp.step, out, getattr(samp, "active", None))
 
     def gather_rows(self, x, idx):
         return x.index_select(0, idx.long())

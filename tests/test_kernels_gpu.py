@@ -473,9 +473,13 @@ def test_sampler(C):
     # decode-step form: same draw written into a slice, counters advanced in-kernel
     buf = torch.full((B + 3,), -1, dtype=torch.int32, device=DEV)
     st2 = step.clone()
-    C.sample_into(logits, V, temp, topk, greedy, seeds, st2, buf[:B])
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st2, buf[:B], None)
     assert buf[:B].cpu().tolist() == exp.tolist() and buf[B:].cpu().tolist() == [-1] * 3
     assert torch.equal(st2, step + 1)
+    act = (torch.arange(B, device=DEV) % 3 != 0).int()  # pad rows (0) keep their counter
+    st3 = step.clone()
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st3, buf[:B], act)
+    assert buf[:B].cpu().tolist() == exp.tolist() and torch.equal(st3, step + act)
     for r in range(B):
         k = 1 if greedy[r] else int(topk[r])
         assert int(out[r]) in set(torch.topk(logits[r, :V], k).indices.tolist())
@@ -510,6 +514,10 @@ def test_sampler_fast_path_and_ties(C, case):
     # decode-step form: same draw written into a slice, counters advanced in-kernel
     buf = torch.full((B + 3,), -1, dtype=torch.int32, device=DEV)
     st2 = step.clone()
-    C.sample_into(logits, V, temp, topk, greedy, seeds, st2, buf[:B])
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st2, buf[:B], None)
     assert buf[:B].cpu().tolist() == exp.tolist() and buf[B:].cpu().tolist() == [-1] * 3
     assert torch.equal(st2, step + 1)
+    act = (torch.arange(B, device=DEV) % 3 != 0).int()  # pad rows (0) keep their counter
+    st3 = step.clone()
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st3, buf[:B], act)
+    assert buf[:B].cpu().tolist() == exp.tolist() and torch.equal(st3, step + act)
