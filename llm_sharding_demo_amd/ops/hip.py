@@ -173,6 +173,9 @@ class HipBackend(Backend):
     TILED_ALL_M = int(os.environ.get("LSD_TILED_ALL_M", "128"))
     # workgroup target of split-K residual GEMMs on the ring (0 = TILED3_MAX)
     RING_RESID_TARGET = int(os.environ.get("LSD_RING_RESID_TARGET", "256"))
+    # 128x128-tile target of residual projections for decode groups of
+    # 257-1024 rows (0 = the prefill rule, ~256 tiles); see _resid_splits
+    RESID_WG_TARGET = int(os.environ.get("LSD_RESID_WG_TARGET", "1024"))
     TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
     TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4000"))
 
@@ -248,6 +251,14 @@ class HipBackend(Backend):
                 target = min(self.TILED3_MAX, self.RING_RESID_TARGET or self.TILED3_MAX)
                 return max(1, min(target // tiles, K // 512 or 1))
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
+            if M <= 1024 and self.RESID_WG_TARGET:
+                # decode groups above 256 rows: ~RESID_WG_TARGET 128x128 tiles,
+                # at most one split per 1024 of K (at least 2).  512 rows, GEMM +
+                # slab-folding norm (profiles/r2_resid512_splits.log): Llama-3 8B
+                # down 119.7 -> 81.5 us, o-proj 44.2 -> 38.7; GPT-2 XL MLP-down
+                # 54.7 -> 32.2 (the old rule gave 2 splits on the 128x64 ring)
+                return max(1, min(math.ceil(self.RESID_WG_TARGET / tiles), max(2, K // 1024),
+                                  K // 64 // 2 or 1))
             return max(1, min(math.ceil(256 / tiles), K // 64 // 2 or 1))
         if self.DEFER_RESID:
             # deferred slabs cost S x M x N x 4 B of writes + norm reads, so

@@ -272,6 +272,28 @@ def test_big_gemm_epilogues(BIG, CNT, M, K):
         close(x, x_ref, 2e-3, 1e-3)
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 1600, 6400), (512, 4096, 4096), (384, 1600, 1600)])
+@pytest.mark.parametrize("splits", [2, 4, 6, 8])
+def test_resid_splits_above_256_rows(C, CNT, M, N, K, splits):
+    """Residual projections of 257-1024-row decode groups with the K-split
+    counts _resid_splits now picks (default routing: 128x64 ring, 128x128
+    tiled or the 256x256 p8 kernel, depending on the grid), slabs folded by
+    the norm, against the fp32 reference."""
+    a, w, bias = bf(M, K, seed=70), bf(N, K, scale=0.02, seed=71), bf(N, scale=0.1, seed=72)
+    C.gemm_set_tiled3_max(512)  # the engine's routing (HipBackend defaults)
+    C.gemm_set_ring_tn(0)
+    try:
+        x = torch.randn(M, N, device=DEV)
+        x_ref = x + ref.linear(a, w, bias)
+        slab = C.linear_residual(a, w, bias, x, splits, True, CNT, True)
+        assert slab is not None and slab.shape == (splits, M, N)
+        C.norm(x, slab, bias, None, None, 0.0, True, None, False)
+        close(x, x_ref, 3e-3, 2e-3)
+    finally:
+        C.gemm_set_tiled3_max(0)
+        C.gemm_set_ring_tn(128)
+
+
 def _cache(slots, n_kv, S, hd):
     return (torch.zeros(slots, n_kv, S, hd, dtype=torch.bfloat16, device=DEV),
             torch.zeros(slots, n_kv, S, hd, dtype=torch.bfloat16, device=DEV))
