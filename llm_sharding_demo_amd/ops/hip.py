@@ -176,6 +176,8 @@ class HipBackend(Backend):
     # 128x128-tile target of residual projections for decode groups of
     # 257-1024 rows (0 = the prefill rule, ~256 tiles); see _resid_splits
     RESID_WG_TARGET = int(os.environ.get("LSD_RESID_WG_TARGET", "1024"))
+    # 8 K splits for K >= 8192 residual projections of 129-256 rows (0 = off)
+    RESID_LONGK = int(os.environ.get("LSD_RESID_LONGK", "1"))
     TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
     TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4000"))
 
@@ -247,6 +249,12 @@ class HipBackend(Backend):
                 # to the slab combine than they gain in workgroups (GPT-2 XL
                 # attention out-proj, K = 1600: 3 splits 11.8 us vs 5 splits
                 # 12.6 at 256 rows, 9.2 vs 9.3 at 128; profiles/r2_ring_tn32.log)
+                if M > 128 and K >= 8192 and self.RESID_LONGK:
+                    # long-K projections above 128 rows: 8 splits, which leaves
+                    # the ring for the 128x128 tiled kernel -- Llama-3 8B down at
+                    # 256 rows 71.9 -> 55.3 us with its norm (2 ring splits);
+                    # profiles/r2_resid512_splits.log
+                    return min(8, K // 1024)
                 tiles = math.ceil(M / 128) * math.ceil(N / 64)
                 target = min(self.TILED3_MAX, self.RING_RESID_TARGET or self.TILED3_MAX)
                 return max(1, min(target // tiles, K // 512 or 1))

@@ -272,7 +272,7 @@ def test_big_gemm_epilogues(BIG, CNT, M, K):
         close(x, x_ref, 2e-3, 1e-3)
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 1600, 6400), (512, 4096, 4096), (384, 1600, 1600)])
+@pytest.mark.parametrize("M,N,K", [(512, 1600, 6400), (512, 4096, 4096), (384, 1600, 1600), (256, 1024, 8192)])
 @pytest.mark.parametrize("splits", [2, 4, 6, 8])
 def test_resid_splits_above_256_rows(C, CNT, M, N, K, splits):
     """Residual projections of 257-1024-row decode groups with the K-split
