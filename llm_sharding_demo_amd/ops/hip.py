@@ -178,6 +178,7 @@ class HipBackend(Backend):
     RESID_WG_TARGET = int(os.environ.get("LSD_RESID_WG_TARGET", "1024"))
     # 8 K splits for K >= 8192 residual projections of 129-256 rows (0 = off)
     RESID_LONGK = int(os.environ.get("LSD_RESID_LONGK", "1"))
+    RESID_LONGK_MIN_M = int(os.environ.get("LSD_RESID_LONGK_MIN_M", "128"))
     TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
     TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4000"))
 
@@ -249,7 +250,7 @@ class HipBackend(Backend):
                 # to the slab combine than they gain in workgroups (GPT-2 XL
                 # attention out-proj, K = 1600: 3 splits 11.8 us vs 5 splits
                 # 12.6 at 256 rows, 9.2 vs 9.3 at 128; profiles/r2_ring_tn32.log)
-                if M > 128 and K >= 8192 and self.RESID_LONGK:
+                if M > self.RESID_LONGK_MIN_M and K >= 8192 and self.RESID_LONGK:
                     # long-K projections above 128 rows: 8 splits, which leaves
                     # the ring for the 128x128 tiled kernel -- Llama-3 8B down at
                     # 256 rows 71.9 -> 55.3 us with its norm (2 ring splits);
