@@ -333,7 +333,17 @@ extern "C" int lsd_gemv_ok(int M, int K, int epi, int norm) {
   if (mr * nb > 16) return 0;
   if (norm != gv::NONE && mr * nb > 4) return 0;
   if (epi == 5) return 0;  // no slab epilogue: the GEMV never splits K
-  return 1;
+  // exactly the (epilogue, norm) pairs lsd_gemv dispatches: a pair it does not
+  // instantiate must read "not ok" so the caller materialises the norm first
+  switch (epi * 4 + norm) {
+    case gv::BF16 * 4 + gv::NONE: case gv::GELU * 4 + gv::NONE: case gv::GELU * 4 + gv::LN:
+    case gv::SILU * 4 + gv::NONE: case gv::SILU * 4 + gv::RMS: case gv::F32 * 4 + gv::NONE:
+    case gv::F32 * 4 + gv::LN: case gv::F32 * 4 + gv::RMS: case gv::RESID * 4 + gv::NONE:
+    case gv::QKV * 4 + gv::NONE: case gv::QKV * 4 + gv::LN: case gv::QKV * 4 + gv::RMS:
+      return 1;
+    default:
+      return 0;
+  }
 }
 
 static int g_gemv_nt = 0;

@@ -200,10 +200,14 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     int cnt = 0;
     unsigned long long msk = 0;
     if (one) {
+      // padding past V (-inf in registers) never becomes a candidate: with
+      // fewer than k segments holding real logits (V < ~4096) tau is -inf and
+      // would otherwise admit it, and its index lies past the row's end
 #pragma unroll
       for (int i = 0; i < CH; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) msk |= q[i][j] >= tau ? (1ull << (4 * i + j)) : 0ull;
+        for (int j = 0; j < 4; ++j)
+          msk |= (q[i][j] >= tau && (tid + i * NT) * 4 + j < V) ? (1ull << (4 * i + j)) : 0ull;
       cnt = __popcll(msk);
     } else {
       for_row(x, V, [&](float val, int) { cnt += val >= tau ? 1 : 0; });

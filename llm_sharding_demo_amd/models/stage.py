@@ -136,6 +136,7 @@ class StageModel:
         group's parity under alternating splits; 0 otherwise)."""
         x = self.embed(inp, meta) if self.first else inp
         r = Residual(x)
+        self.backend.decode = meta.is_decode  # decode-only routing rules (ops/hip.py)
         gpt2 = self.cfg.arch == "gpt2"
         attn_fn = self._gpt2_attn if gpt2 else self._llama_attn
         mlp_fn = self._gpt2_mlp if gpt2 else self._llama_mlp

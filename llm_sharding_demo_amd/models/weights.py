@@ -135,7 +135,16 @@ def _stage_tensor_shapes(cfg: ModelConfig, layers: Iterable[int], first: bool, l
 
 def _init_one(cfg: ModelConfig, name: str, shape, seed: int, device, dtype) -> torch.Tensor:
     base = name.rsplit(".", 1)[-1]
-    if name in ("wte", "embed_tokens", "lm_head"):
+    if name == "embed_tokens":
+        # untied (Llama) input embeddings at unit scale (the T5 / muP
+        # convention: the residual stream enters at the RMS its norms produce).
+        # With HF's 0.02 the first layers' outputs dwarf the stream and random
+        # -init depth amplifies bf16 rounding: fp32 vs bf16-emulated logits at
+        # 32 layers, H = 2048: 6.6 % -> 1.1 % of the logit std; H = 1024: 3.3 %
+        # -> 0.7 % (profiles/r3_llama_init_depth.log).  Residual projections
+        # below are depth-scaled (0.02 / sqrt(2L)) as in GPT-2 / Llama training.
+        return _randn(shape, 1.0, seed, name, device, dtype)
+    if name in ("wte", "lm_head"):
         return _randn(shape, 0.02, seed, name, device, dtype)
     if name == "wpe":
         return _randn(shape, 0.01, seed, name, device, dtype)

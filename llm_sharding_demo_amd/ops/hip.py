@@ -203,10 +203,20 @@ class HipBackend(Backend):
     def prepare_stage(self, stage) -> None:
         cfg, w, dev = stage.cfg, stage.w, stage.device
         if stage.last:
-            head = w["wte"] if cfg.arch == "gpt2" else w["lm_head"]
-            pad = torch.zeros(cfg.vocab_padded, cfg.hidden, dtype=head.dtype, device=dev)
-            pad[: cfg.vocab_size] = head
-            stage._lm_head_padded = pad
+            # pad the head IN PLACE: the stage keeps one [vocab_padded, H]
+            # tensor and its weight dict points at the first V rows (a
+            # contiguous view -- the tied GPT-2 embedding of a 1-stage pipeline
+            # reads the same rows), so the unpadded copy is freed
+            key = "wte" if cfg.arch == "gpt2" else "lm_head"
+            head = w[key]
+            if head.shape[0] == cfg.vocab_padded:
+                stage._lm_head_padded = head
+            else:
+                pad = torch.zeros(cfg.vocab_padded, cfg.hidden, dtype=head.dtype, device=dev)
+                pad[: cfg.vocab_size] = head
+                w[key] = pad[: cfg.vocab_size]
+                del head
+                stage._lm_head_padded = pad
         if cfg.arch == "llama":
             perm_q = rope_pair_permutation(cfg.n_heads, cfg.head_dim)
             perm_k = rope_pair_permutation(cfg.n_kv_heads, cfg.head_dim) + cfg.q_size
@@ -260,7 +270,9 @@ class HipBackend(Backend):
                 target = min(self.TILED3_MAX, self.RING_RESID_TARGET or self.TILED3_MAX)
                 return max(1, min(target // tiles, K // 512 or 1))
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
-            if M <= 1024 and self.RESID_WG_TARGET:
+            # decode groups only: a 257-1024-token prefill chunk keeps the
+            # prefill rule below (the target was measured on decode steps)
+            if M <= 1024 and self.RESID_WG_TARGET and getattr(self, "decode", True):
                 # decode groups above 256 rows: ~RESID_WG_TARGET 128x128 tiles,
                 # at most one split per 1024 of K (at least 2).  512 rows, GEMM +
                 # slab-folding norm (profiles/r2_resid512_splits.log): Llama-3 8B

@@ -188,15 +188,21 @@ class Engine:
         dist mode every rank computes its own cap and all take the minimum."""
         want = self.cfg.max_batch
         fits = want
+        # stages sharing a device (the 1-GPU loopback rehearsal) share its HBM:
+        # sum their weights and their KV layers (every stage holds the same
+        # slot count) before sizing the slots against that device's budget
+        per_dev: dict = {}
         for i, dev in enumerate(devices):
             if dev.type != "cuda":
                 continue
-            # the stage's KV layers (its attention halves)
-            a, b = self.unit_plan[self.stage_idx if collective else i]
-            n_kv_layers = sum(1 for u in range(a, b) if u % 2 == 0)
-            per_stage_w = self._weight_bytes(self.stage_idx if collective else i)
+            si = self.stage_idx if collective else i
+            a, b = self.unit_plan[si]  # the stage's KV layers: its attention halves
+            acc = per_dev.setdefault(str(dev), [dev, 0, 0])
+            acc[1] += sum(1 for u in range(a, b) if u % 2 == 0)
+            acc[2] += self._weight_bytes(si)
+        for dev, n_kv_layers, w_bytes in per_dev.values():
             fits = min(fits, plan_slots(want + 2, n_kv_layers, self.mcfg.n_kv_heads, self.max_seq,
-                                        self.mcfg.head_dim, dev, reserve=per_stage_w,
+                                        self.mcfg.head_dim, dev, reserve=w_bytes,
                                         fraction=self.cfg.kv_fraction) - 2)
         if collective:
             import torch.distributed as dist
@@ -217,8 +223,10 @@ class Engine:
         n = per_layer * (b - a) // 2
         if i == 0:
             n += mc.embed_params() * 2
-        if i == self.P - 1:
-            n += mc.lm_head_params() * 2 * 2  # weight + padded copy
+        if i == self.P - 1 and not (i == 0 and mc.tie_embeddings):
+            # the head, padded in place (ops/hip.py prepare_stage); a tied
+            # GPT-2 head on a 1-stage pipeline is the embedding counted above
+            n += mc.lm_head_params() * 2
         return n
 
     def _build_stage(self, i: int, device: torch.device) -> StageModel:
@@ -488,6 +496,9 @@ class Engine:
         self._tok_q.put((plan.step, (plan.replica, plan.step, gp.g), host, ev))
 
     def _tok_shipper(self) -> None:
+        # test hook: hold replica readouts back so they land after rank 0's
+        # own session has nothing left to plan (tests/test_pipeline.py)
+        delay = float(os.environ.get("LSD_TEST_TOK_DELAY_S", "0"))
         while True:
             item = self._tok_q.get()
             if item is None:
@@ -497,6 +508,8 @@ class Engine:
             step, key, host, ev = item
             if ev is not None:
                 ev.synchronize()
+            if delay:
+                time.sleep(delay)
             self.tok_ch.send(0, (step, key, host.tolist()))
 
     def _tok_receiver(self, rep: int) -> None:

@@ -480,7 +480,11 @@ class Scheduler:
             self.core.add(i, len(req.prompt_ids), p.max_new_tokens, bool(p.stop_at_eos))
 
     def has_work(self) -> bool:
-        return bool(self.queue.depth) or self.core.has_work()
+        """Anything left to plan OR to read back: token readouts still queued
+        here, or expected by the core (replica > 0 readouts arrive later over
+        the control plane), keep a serving session alive until they land."""
+        return (bool(self.queue.depth) or self.core.has_work() or bool(self.readouts)
+                or self.core.n_expect > 0)
 
     # -- plan building ---------------------------------------------------------
     def build_step(self) -> Optional[List[StepPlan]]:

@@ -543,3 +543,29 @@ def test_sampler_fast_path_and_ties(C, case):
     st3 = step.clone()
     C.sample_into(logits, V, temp, topk, greedy, seeds, st3, buf[:B], act)
     assert buf[:B].cpu().tolist() == exp.tolist() and torch.equal(st3, step + act)
+
+
+@pytest.mark.parametrize("V,Vp", [(1000, 1024), (1000, 1000), (3000, 3008)])
+def test_sampler_small_vocab(C, V, Vp):
+    """V < 4096 (the test presets): fewer than k of the 64 segments hold real
+    logits, so the fast path's threshold is -inf -- padding past V must never
+    become a candidate (its index lies past the row).  The rows sit
+    at the very end of their allocation so an over-read would leave it."""
+    from llm_sharding_demo_amd.runtime.batch import counter_uniform
+
+    B = 4
+    g = torch.Generator(device=DEV).manual_seed(9)
+    store = torch.empty(B * Vp, device=DEV)  # exact size: nothing after the last row
+    logits = store.view(B, Vp)
+    logits.copy_(torch.randn(B, Vp, device=DEV, generator=g) * 2)
+    logits[:, V:] = 100.0
+    temp = torch.tensor([0.6, 1.0, 0.6, 1.0], device=DEV)
+    topk = torch.tensor([20, 40, 64, 40], dtype=torch.int32, device=DEV)
+    greedy = torch.zeros(B, dtype=torch.int32, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 31 + 1
+    step = torch.arange(B, dtype=torch.int64, device=DEV)
+    out = C.sample(logits, V, temp, topk, greedy, seeds, step)
+    exp = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), greedy.cpu(),
+                     counter_uniform(seeds.cpu(), step.cpu()), V)
+    assert out.cpu().tolist() == exp.tolist()
+    assert all(0 <= t < V for t in out.cpu().tolist())

@@ -176,6 +176,47 @@ def test_gloo_multiprocess_pipeline(golden, tmp_path, world, dp, chunk):
     assert out2 == golden[:2]
 
 
+def test_gloo_dp_serving_loop_finishes_every_replica(golden, tmp_path):
+    """dp = 2 under the serving loop (start_loop): one request lands on each
+    replica; replica 1's tokens reach rank 0 over the control plane after
+    replica 0's session has nothing left to plan -- every request must still
+    finish without any further traffic (readouts kept the session
+    alive only when local)."""
+    script = tmp_path / "w.py"
+    script.write_text(textwrap.dedent(f"""
+        import sys, json, time, torch
+        sys.path.insert(0, {ROOT!r})
+        from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
+        from llm_sharding_demo_amd.runtime.engine import build_engine
+        cfg = EngineConfig(model_id="gpt2-test", max_batch=4, device="cpu", transport="gloo",
+                           num_microbatches=1, dp_replicas=2)
+        eng = build_engine(cfg)
+        if eng.rank != 0:
+            eng.worker_loop()
+        else:
+            eng.start_loop()
+            reqs = [eng.submit(p, SamplingParams(greedy=True, max_new_tokens=6))
+                    for p in {PROMPTS!r}[:2]]
+            t0 = time.monotonic()
+            out = [r.wait(60) for r in reqs]
+            dt = time.monotonic() - t0
+            eng.shutdown()
+            print("RESULT", json.dumps([out, dt]))
+    """))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               OMP_NUM_THREADS="1", LSD_TEST_TOK_DELAY_S="0.3")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={env['MASTER_PORT']}", str(script)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")][0]
+    out, dt = json.loads(line[len("RESULT "):])
+    assert out == golden[:2]
+    assert dt < 30
+
+
 def test_gloo_compat_forwards_in_dist_mode(tmp_path):
     """/forward and /forward_b served by a torchrun engine (role `all`): stage
     0's output on rank 0, the rest of the pipeline over the pipeline edges;
