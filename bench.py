@@ -167,12 +167,19 @@ def main() -> int:
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    ranks = None
     if N > 1:
         import torch.distributed as dist
 
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=eng.transport.ctrl)
         elapsed = float(t[0])
+        # data-plane evidence from every rank: what the process group and the
+        # transport saw (world size, device, communicators this rank joined)
+        me = {"rank": eng.rank, "replica": eng.replica, "stage": eng.stage_idx,
+              "device": str(eng.devices[0]), "pg_world": dist.get_world_size(),
+              "comms": eng.transport.num_comms}
+        ranks = eng.transport.gather_object(me, dst=0)
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
         tokens = B * args.gen * args.steps
@@ -185,6 +192,8 @@ def main() -> int:
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / base, 1) if base else None,
+            "vs_baseline_note": "vs the reference's own CPU fp32 HTTP code path (survey-measured, "
+                                "BASELINE.md); the reference publishes no number: not a like-for-like speedup",
             "dtype": "bf16" if args.device != "cpu" else "fp32",
             "data": "synthetic prompts, random-init weights",
             "p50_token_latency_ms": round(p50, 4) if p50 is not None else None,
@@ -200,8 +209,14 @@ def main() -> int:
                        "sampler": "greedy" if args.greedy else "T0.6/top-k40",
                        "hipgraphs": not args.no_graphs},
         }
-        if args.loopback_stages and eng.last_session is not None:
+        if (args.loopback_stages or N > 1) and eng.last_session is not None:
             out["stage_busy"] = [st["busy_fraction"] for st in eng.last_session.stages]
+        if N > 1 or args.loopback_stages:
+            out["transport"] = transport
+        if ranks is not None:
+            out["pg_world_size"] = ranks[0]["pg_world"]
+            out["data_plane_comms"] = sum(r["comms"] for r in ranks)
+            out["rank_devices"] = [r["device"] for r in ranks]
         print(json.dumps(out), flush=True)
         hp = getattr(eng, "_hostprof", None)
         if hp is not None and hp[3]:

@@ -26,6 +26,8 @@ void lsd_gemm_set_ring_slots(int v);
 void lsd_gemm_set_ring_tn(int v);
 void lsd_gemm_set_ring_fill(int v);
 void lsd_gemm_set_ring_m96(int v);
+void lsd_gemm_set_d256_slots(int v);
+int lsd_gemm_d256_bn(int kind, int M, int N, int K);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
 void lsd_attn_set_large_waves(int hd, int v);
@@ -97,7 +99,7 @@ const bf16* opt_bias(const c10::optional<torch::Tensor>& b, int N) {
   return bptr(*b);
 }
 
-GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, bool tiled) {
+GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, int64_t tiled) {
   need(a, torch::kBFloat16, "a");
   need(w, torch::kBFloat16, "w");
   need_rows(a, "a");
@@ -109,6 +111,9 @@ GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, bool tile
   p.M = a.size(0); p.N = w.size(0); p.K = a.size(1);
   p.splits = 1;
   TORCH_CHECK(p.N % 16 == 0, "N must be a multiple of 16 (pad the weight), got ", p.N);
+  TORCH_CHECK(tiled >= 0 && tiled <= 3, "GEMM kind must be 0 (split-K), 1 (tiled), 2 / 3 (256-row), got ", tiled);
+  if (tiled >= 2)
+    TORCH_CHECK(p.M >= 1 && p.M <= 256, "256-row decode GEMM needs 1 <= M <= 256, got ", p.M);
   if (tiled) {
     TORCH_CHECK(p.K % 64 == 0, "tiled GEMM needs K % 64 == 0, got ", p.K);
   } else {
@@ -121,7 +126,7 @@ GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, bool tile
 
 // Launch with split-K bookkeeping: the decode path needs persistent zeroed
 // ticket counters (one per column tile) and an fp32 partial-tile workspace.
-void run_gemm(GemmParams& p, int epi, bool tiled, int64_t splits,
+void run_gemm(GemmParams& p, int epi, int64_t tiled, int64_t splits,
               const c10::optional<torch::Tensor>& counters, const torch::Tensor& like,
               const char* what) {
   const int kt = tiled ? p.K / 64 : p.K / 32;
@@ -130,6 +135,21 @@ void run_gemm(GemmParams& p, int epi, bool tiled, int64_t splits,
   int* cnt = nullptr;
   float* ws = nullptr;
   torch::Tensor wsbuf;
+  if (tiled && splits > 1 && epi != EPI_SLAB) {
+    // tiled split-K with an in-kernel combine: only the 256-row decode kernel
+    // (gemm_d256) has one -- ticket counters + fp32 partial tiles per split
+    const int bn = lsd_gemm_d256_bn((int)tiled, p.M, p.N, p.K);
+    TORCH_CHECK(bn > 0, what, ": tiled split-K with an in-kernel combine needs the 256-row kernel (kind 2 / 3)");
+    const long tiles = (p.N + bn - 1) / bn;
+    TORCH_CHECK(counters.has_value(), what, ": split-K needs the ticket counter buffer");
+    need(*counters, torch::kInt32, "counters");
+    TORCH_CHECK(counters->is_contiguous() && counters->numel() >= tiles,
+                what, ": counter buffer too small (", counters->numel(), " < ", tiles, ")");
+    cnt = counters->data_ptr<int>();
+    TORCH_CHECK(splits * 256L * bn * 4 < (1L << 31), what, ": split workspace too large");
+    wsbuf = torch::empty({tiles * splits * 256 * bn}, like.options().dtype(torch::kFloat32));
+    ws = wsbuf.data_ptr<float>();
+  }
   if (!tiled && epi != EPI_SLAB) {
     const int nw = lsd_gemm_sk_nw(p.M, epi);  // column tile = 64 * nw (partial last tile masked)
     if (epi == EPI_SILU_MUL)
@@ -149,13 +169,13 @@ void run_gemm(GemmParams& p, int epi, bool tiled, int64_t splits,
     }
   }
   p.stamps = g_stamps;
-  check_hip(lsd_gemm(&p, epi, tiled ? 1 : 0, cnt, ws, cur_stream()), what);
+  check_hip(lsd_gemm(&p, epi, (int)tiled, cnt, ws, cur_stream()), what);
 }
 
 
 // out = act(a @ w^T + bias), bf16
 torch::Tensor linear(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,
-                     int64_t act, bool tiled, int64_t splits,
+                     int64_t act, int64_t tiled, int64_t splits,
                      c10::optional<torch::Tensor> counters) {
   GemmParams p = base_params(a, w, tiled);
   p.bias = opt_bias(bias, p.N);
@@ -170,7 +190,7 @@ torch::Tensor linear(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tens
 }
 
 // fp32 logits = a @ w^T
-torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, bool tiled, int64_t splits,
+torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, int64_t tiled, int64_t splits,
                          c10::optional<torch::Tensor> counters) {
   GemmParams p = base_params(a, w, tiled);
   auto out = torch::empty({p.M, p.N}, a.options().dtype(torch::kFloat32));
@@ -185,7 +205,7 @@ torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, bool tiled, int64_t s
 // slabs [splits, M, N] (bias not applied) that the next norm folds in.
 c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
                                               c10::optional<torch::Tensor> bias, torch::Tensor x,
-                                              int64_t splits, bool tiled,
+                                              int64_t splits, int64_t tiled,
                                               c10::optional<torch::Tensor> counters, bool defer) {
   GemmParams p = base_params(a, w, tiled);
   need(x, torch::kFloat32, "x");
@@ -209,7 +229,7 @@ c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
 torch::Tensor linear_qkv(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,
                          torch::Tensor kc, torch::Tensor vc, torch::Tensor tslot,
                          torch::Tensor tpos, int64_t q_size, int64_t kv_size, int64_t hd,
-                         c10::optional<torch::Tensor> rope, bool tiled, int64_t splits,
+                         c10::optional<torch::Tensor> rope, int64_t tiled, int64_t splits,
                          c10::optional<torch::Tensor> counters) {
   GemmParams p = base_params(a, w, tiled);
   p.bias = opt_bias(bias, p.N);
@@ -562,6 +582,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_ring_tn", [](int64_t v) { lsd_gemm_set_ring_tn((int)v); });
   m.def("gemm_set_ring_fill", [](int64_t v) { lsd_gemm_set_ring_fill((int)v); });
   m.def("gemm_set_ring_m96", [](int64_t v) { lsd_gemm_set_ring_m96((int)v); });
+  // gemm_d256 (launch kind 2 / 3: all <= 256 rows in one tile, 64 / 128 columns): ring depth
+  m.def("gemm_set_d256_slots", [](int64_t v) { lsd_gemm_set_d256_slots((int)v); });
+  m.def("gemm_d256_bn", [](int64_t kind, int64_t M, int64_t N, int64_t K) {
+    return lsd_gemm_d256_bn((int)kind, (int)M, (int)N, (int)K);
+  });
   // decode attention: cap the grid (blocks loop over (sequence, head) items)
   m.def("attn_set_max_wg", [](int64_t v) { lsd_attn_set_max_wg((int)v); });
   // decode attention: waves per block when the batch has few (sequence, head) items

@@ -37,6 +37,8 @@ struct Rccl {
   ncclResult_t (*group_end)() = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   ncclResult_t (*get_version)(int*) = nullptr;
+  ncclResult_t (*get_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
 };
 
 const Rccl& rccl() {
@@ -61,6 +63,8 @@ const Rccl& rccl() {
     r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
     r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
     r.get_version = reinterpret_cast<decltype(r.get_version)>(sym("ncclGetVersion"));
+    r.get_async_error = reinterpret_cast<decltype(r.get_async_error)>(sym("ncclCommGetAsyncError"));
+    r.comm_abort = reinterpret_cast<decltype(r.comm_abort)>(sym("ncclCommAbort"));
   });
   return r;
 }
@@ -108,6 +112,26 @@ void lsd_register_comm(py::module& m) {
     return reinterpret_cast<int64_t>(c);
   });
   m.def("rccl_comm_destroy", [](int64_t h) { check(rccl().comm_destroy(as_comm(h)), "ncclCommDestroy"); });
+  // Failure handling: the communicator's asynchronous error
+  // state (ncclSuccess = 0, ncclInProgress = 7 while a non-blocking init or
+  // abort runs; anything else is a failed peer / network / internal error),
+  // polled by the engine watchdog ...
+  m.def("rccl_async_error", [](int64_t h) {
+    ncclResult_t e = ncclSuccess;
+    check(rccl().get_async_error(as_comm(h), &e), "ncclCommGetAsyncError");
+    return (int)e;
+  });
+  m.def("rccl_error_string", [](int code) { return std::string(rccl().error_string((ncclResult_t)code)); });
+  // ... and the way out of a hang: ncclCommAbort sets the communicator's
+  // abort flag, which every RCCL kernel of it polls in its wait loops, so an
+  // unmatched ncclRecv / ncclSend (a dead or stalled peer) returns and the
+  // streams behind it drain.  Frees the communicator (do not destroy after).
+  // Called from the watchdog thread while another thread may be blocked in a
+  // stream / event synchronize on work of this communicator.
+  m.def("rccl_comm_abort", [](int64_t h) {
+    py::gil_scoped_release nogil;
+    check(rccl().comm_abort(as_comm(h)), "ncclCommAbort");
+  });
   // Byte-wise send / receive of a dense tensor on the CURRENT stream.
   m.def("rccl_send", [](int64_t h, torch::Tensor t, int peer) {
     need_dense(t, "rccl_send");

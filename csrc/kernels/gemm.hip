@@ -1184,6 +1184,218 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
 }
 
 // ---------------------------------------------------------------------------
+// Decode GEMM at 129-256 rows: every row in ONE 256 x BN tile, 8 waves
+// ---------------------------------------------------------------------------
+// The 128x64 ring tiles above read the whole A operand once per column tile
+// AND once per 128-row block; at 256 rows that A traffic (L2 -> CU) is 2/3 of
+// the bytes a workgroup moves, and the ring runs at ~38 GB/s per CU
+// (profiles/r2_decode_gemm_limits.log).  Here a workgroup owns all <= 256
+// rows of BN columns (guide §5 "Projection GEMM at M = 256": BN = 64 x all
+// rows, 8 waves as 8 (M) x 1 (N), split-K so that (N / BN) x S ~ the CU
+// count): 0.83x (BN 64) / 0.58x (BN 128) the operand bytes per output of the
+// 128x64 ring, and twice the waves per CU to keep the loads and the MFMAs of
+// consecutive k-steps overlapped.
+//   * wave w owns rows [32 w, 32 w + 32) x all BN columns: 2 x BN/16 MFMA
+//     tiles (v_mfma_f32_16x16x32_bf16), fp32 accumulators;
+//   * k-step = 64: A [256][64] (32 KiB) and W [BN][64] staged by LDS-DMA
+//     (global_load_lds, 16 B per lane, full 128-B lines, XOR-swizzled on the
+//     source address -- the ring kernel's conflict-free image), SLOTS-deep
+//     ring, counted vmcnt + one raw s_barrier per step (as gemm_ring_kernel);
+//   * S > 1 K splits: EPI_SLAB writes its partial slab (the residual
+//     projections: the next norm folds the S slabs, bindings linear_residual);
+//     every other epilogue publishes its fp32 partial tile write-through (sc1
+//     stores, sc1 loads: guide §5 "In-launch split-K reduction", sc1 form) and
+//     the last-arriving split sums the S partials in split order
+//     (deterministic) and runs the fused epilogue.  A tile's splits have
+//     consecutive remapped ids, so they share an XCD (speed only).
+template <int ROWS>
+__device__ __forceinline__ void stage8(char* lds_tile, const bf16* src, long ld, int row0, int row_max,
+                                       int k0) {
+  // 8 waves: ROWS / 64 wave-instructions of 1 KiB (8 rows x 128 B) each, the
+  // [ROWS][64 k] image with 16-B chunks swizzled by (row >> 1) & 7 (lds_frag)
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  constexpr int PER_WAVE = ROWS / 64;
+#pragma unroll
+  for (int q = 0; q < PER_WAVE; ++q) {
+    const int inst = w * PER_WAVE + q;
+    const int row = inst * 8 + (lane >> 3);
+    const int lch = (lane & 7) ^ ((row >> 1) & 7);
+    const bf16* gp = src + (long)min(row0 + row, row_max) * ld + k0 + lch * 8;
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)gp, (lds_void*)(lds_tile + inst * 1024), 16, 0, 0);
+  }
+}
+
+template <int BN, int SLOTS>
+constexpr int d256_smem() {
+  return SLOTS * (256 + BN) * 128 > 256 * (BN + 4) * 4 ? SLOTS * (256 + BN) * 128 : 256 * (BN + 4) * 4;
+}
+
+template <int EPI, int BN, int SLOTS>
+__global__ __launch_bounds__(512) void gemm_d256_kernel(GemmParams p, int* __restrict__ cnt,
+                                                        float* __restrict__ ws) {
+  constexpr int NJ = BN / 16;                 // 16-column MFMA tiles per wave
+  constexpr int A_BYTES = 256 * 64 * 2;       // 32 KiB
+  constexpr int SLOT_BYTES = A_BYTES + BN * 64 * 2;
+  constexpr int LPS = 4 + BN / 64;            // glds per thread per k-step (A + W)
+  constexpr int D = SLOTS - 1;                // k-steps in flight
+  constexpr int SMEM = d256_smem<BN, SLOTS>();
+  static_assert(SLOTS >= 2 && SLOTS <= 4 && SLOTS * SLOT_BYTES <= 160 * 1024, "LDS ring");
+  static_assert((D - 1) * LPS <= 63, "vmcnt range");
+  // ONE __shared__ array: a second LDS object can make hipcc drain the glds
+  // every k-step (guide §5 trap 4(a)).  The reducer flag lives in the ring,
+  // dead by then (all glds waited, every wave past the publish barrier).
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  int* s_flag = reinterpret_cast<int*>(smem);
+
+  const int S = p.splits;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid / S, split = bid % S;
+  const int n0 = tile * BN;
+  const int KT = p.K / 64;
+  const int kb = (int)((long)KT * split / S), ke = (int)((long)KT * (split + 1) / S);
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  LSD_STAMP(0)
+
+  f32x4 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int kt, int slot) {
+    char* b = smem + slot * SLOT_BYTES;
+    stage8<256>(b, p.A, p.lda, 0, p.M - 1, kt * 64);
+    stage8<BN>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, kt * 64);
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (kb + d < ke) issue(kb + d, d);
+  int slot = 0;
+  for (int kt = kb; kt < ke; ++kt) {
+    // this thread's glds of step kt landed; the later steps stay in flight
+    const int later = min(D - 1, ke - 1 - kt);
+    if (D >= 3 && later >= 2) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * LPS));
+    else if (later == 1) __builtin_amdgcn_s_waitcnt(vmcnt_imm(LPS));
+    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    // publishes every wave's DMA of step kt AND proves every wave is done
+    // reading the slot of step kt - 1, which is refilled right after
+    __builtin_amdgcn_s_barrier();
+    if (kt + D < ke) issue(kt + D, slot == 0 ? SLOTS - 1 : slot - 1);
+    const char* ta = smem + slot * SLOT_BYTES;
+    const char* tw = ta + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[2], wf[NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = lds_frag(ta, w * 32 + i * 16 + r, kk * 4 + g);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) wf[j] = lds_frag(tw, j * 16 + r, kk * 4 + g);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(af[i], wf[j], acc[i][j]);
+    }
+    slot = slot == SLOTS - 1 ? 0 : slot + 1;
+  }
+  LSD_STAMP(1)
+
+  if (S > 1 && EPI != EPI_SLAB) {
+    // ---- publish this split's partial tile (write-through), last arriver
+    // sums all S.  Lane-major slab: thread t's (i, j) accumulator at
+    // ((i * NJ + j) * 512 + t) * 16 B, so every access is 16 contiguous bytes.
+    constexpr int PER_BLOCK = 2 * NJ * 512;  // f32x4 per split tile
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        ws + (long)tile * S * PER_BLOCK * 4, (short)0, S * PER_BLOCK * 16, 0x00020000);
+    const int toff = threadIdx.x * 16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                               split * PER_BLOCK * 16 + (i * NJ + j) * 8192 + toff, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int t = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_flag = (t == S - 1);
+      if (t == S - 1) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (*s_flag == 0) return;
+    LSD_STAMP(2)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // every slab load of a group in flight before the adds (one round trip per
+    // group); clamped index x 0/1 mask, no per-load branch (guide §5 trap (c))
+    constexpr int RG = 16 / NJ;  // splits per group: 32 f32x4 (128 VGPRs) in flight
+    for (int s0 = 0; s0 < S; s0 += RG) {
+      f32x4 v[RG][2][NJ];
+#pragma unroll
+      for (int u = 0; u < RG; ++u) {
+        const int s2 = min(s0 + u, S - 1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            v[u][i][j] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, s2 * PER_BLOCK * 16 + (i * NJ + j) * 8192 + toff,
+                                                             0, 16));
+      }
+#pragma unroll
+      for (int u = 0; u < RG; ++u) {
+        const float msk = (s0 + u < S) ? 1.f : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] += v[u][i][j] * msk;
+      }
+    }
+  }
+
+  // ---- epilogue through LDS: fp32 [256][BN + 4] C tile, then 16-byte
+  // row-contiguous stores (epilogue8); the ring is idle (every glds waited,
+  // every wave past the last barrier below)
+  constexpr int CLD = BN + 4;
+  constexpr int CPR = BN / 8;
+  __syncthreads();
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ct[(w * 32 + i * 16 + 4 * g + q) * CLD + j * 16 + r] = acc[i][j][q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 256 * CPR; c += 512) {
+    const int row = c / CPR, ch = c % CPR, m = row, n = n0 + ch * 8;
+    if (m >= p.M || n >= p.N) continue;
+    const float* src = ct + row * CLD + ch * 8;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if constexpr (EPI == EPI_SILU_MUL) {
+      // interleaved [gate16 | up16] 32-column blocks: a gate chunk pairs with
+      // the up chunk 16 columns right (same tile: BN % 32 == 0)
+      if ((ch & 3) >= 2) continue;
+      const float* up = src + 16;
+      const f32x4 ulo = *reinterpret_cast<const f32x4*>(up);
+      const f32x4 uhi = *reinterpret_cast<const f32x4*>(up + 4);
+      const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
+      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
+    } else {
+      epilogue8<EPI>(p, m, n, v, split);
+    }
+  }
+  LSD_STAMP(3)
+}
+
+// ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
 static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
@@ -1201,6 +1413,7 @@ static int g_ring_slots = 3;  // lsd_gemm_set_ring_slots(): 3 or 4
 static int g_ring_tn = 128;   // lsd_gemm_set_ring_tn(): ring tile columns, 128, 64, 32 or 0 (auto 32/64)
 static int g_ring_fill = 128; // auto: 32-wide tiles below this many 64-wide workgroups
 static int g_ring_m96 = 0;    // lsd_gemm_set_ring_m96(): largest 96-row-tile ring grid (0 = off)
+static int g_d256_slots = 3;  // lsd_gemm_set_d256_slots(): gemm_d256 ring depth 2..4 (BN 128: at most 3)
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
 // with N = H), M > g_sk_rows rows run as ceil(M / g_sk_rows) row blocks
@@ -1256,6 +1469,39 @@ static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_
   } else {
     return sk_nw(p.M, EPI) == 2 ? launch_sk_nw<EPI, 2>(p, cnt, ws, st) : launch_sk_nw<EPI, 1>(p, cnt, ws, st);
   }
+}
+
+// Launch kinds (lsd_gemm `kind`): 0 split-K decode kernel, 1 tiled family
+// (ring / 128x128 / 256x256 by shape), 2 / 3 gemm_d256 with 64 / 128-column
+// tiles (M <= 256, K % 64 == 0; the caller picks it per GEMM).
+static int d256_bn(int kind, int M, int N, int K) {
+  if (kind < 2 || M < 1 || M > 256 || K % 64 != 0) return 0;
+  return kind == 3 && N % 128 == 0 ? 128 : 64;
+}
+
+template <int EPI, int BN>
+static hipError_t launch_d256_bn(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
+  const dim3 grid(((p.N + BN - 1) / BN) * p.splits), block(512);
+  const int slots = BN == 128 ? min(g_d256_slots, 3) : g_d256_slots;
+  switch (slots) {
+    case 2: hipLaunchKernelGGL((gemm_d256_kernel<EPI, BN, 2>), grid, block, 0, st, p, cnt, ws); break;
+    case 4:
+      if constexpr (BN == 64) {
+        hipLaunchKernelGGL((gemm_d256_kernel<EPI, BN, 4>), grid, block, 0, st, p, cnt, ws);
+        break;
+      }
+      [[fallthrough]];
+    default: hipLaunchKernelGGL((gemm_d256_kernel<EPI, BN, 3>), grid, block, 0, st, p, cnt, ws); break;
+  }
+  return hipGetLastError();
+}
+
+template <int EPI>
+static hipError_t launch_d256(const GemmParams& p, int kind, int* cnt, float* ws, hipStream_t st) {
+  const int bn = d256_bn(kind, p.M, p.N, p.K);
+  if (bn == 0) return hipErrorInvalidValue;
+  if (p.splits > 1 && EPI != EPI_SLAB && (cnt == nullptr || ws == nullptr)) return hipErrorInvalidValue;
+  return bn == 128 ? launch_d256_bn<EPI, 128>(p, cnt, ws, st) : launch_d256_bn<EPI, 64>(p, cnt, ws, st);
 }
 
 template <int EPI>
@@ -1332,6 +1578,10 @@ extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; 
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }
 extern "C" void lsd_gemm_set_ring_fill(int v) { g_ring_fill = v; }
 extern "C" void lsd_gemm_set_ring_m96(int v) { g_ring_m96 = v; }
+extern "C" void lsd_gemm_set_d256_slots(int v) { g_d256_slots = v < 2 ? 2 : (v > 4 ? 4 : v); }
+// columns per gemm_d256 tile of a launch of this kind (0: not a d256 launch):
+// the split workspace and ticket counters are sized from it (bindings.cpp)
+extern "C" int lsd_gemm_d256_bn(int kind, int M, int N, int K) { return d256_bn(kind, M, N, K); }
 extern "C" int lsd_gemm_sk_rblocks(int M, int N, int S) { return sk_rblocks(M, N, S); }
 extern "C" int lsd_gemm_sk_rows(int M, int N, int S) {  // rows per row block
   return sk_mt(M, sk_rblocks(M, N, S)) * 16;
@@ -1341,10 +1591,12 @@ extern "C" void lsd_gemm_set_nw2_rows(int v) { g_nw2_rows = v; }
 extern "C" void lsd_gemm_set_sk_rows(int v) { g_sk_rows = v < 16 ? 16 : (v > 128 ? 128 : v); }
 
 // C ABI used by csrc/bindings.cpp; shapes are validated there.
-extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int tiled, int* cnt, float* ws,
+extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int kind, int* cnt, float* ws,
                                hipStream_t st) {
-#define LSD_DISPATCH(E) \
-  case E: return tiled ? launch_tiled<E>(*p, st) : launch_sk<E>(*p, cnt, ws, st);
+#define LSD_DISPATCH(E)                                                                   \
+  case E:                                                                                 \
+    return kind >= 2 ? launch_d256<E>(*p, kind, cnt, ws, st)                              \
+                     : (kind ? launch_tiled<E>(*p, st) : launch_sk<E>(*p, cnt, ws, st));
   switch (epi) {
     LSD_DISPATCH(EPI_BF16)
     LSD_DISPATCH(EPI_GELU)

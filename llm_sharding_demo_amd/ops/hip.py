@@ -180,6 +180,15 @@ class HipBackend(Backend):
     RESID_LONGK = int(os.environ.get("LSD_RESID_LONGK", "1"))
     RESID_LONGK_MIN_M = int(os.environ.get("LSD_RESID_LONGK_MIN_M", "128"))
     TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
+    # Decode GEMMs of 129-256 rows on the 8-wave all-rows kernel (gemm.hip
+    # gemm_d256_kernel): tile columns (64 / 128, 0 = off, the 128x64 ring),
+    # ring depth, and the workgroup targets that set the K splits of the
+    # in-kernel-combined GEMMs (QKV, MLP-up) and of the residual slabs
+    D256 = int(os.environ.get("LSD_D256", "0"))
+    D256_SLOTS = int(os.environ.get("LSD_D256_SLOTS", "3"))
+    D256_TARGET = int(os.environ.get("LSD_D256_TARGET", "192"))
+    D256_RESID_TARGET = int(os.environ.get("LSD_D256_RESID_TARGET", "192"))
+    D256_RESID = int(os.environ.get("LSD_D256_RESID", "0"))  # residual projections too
     TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4000"))
 
     def __init__(self):
@@ -191,6 +200,7 @@ class HipBackend(Backend):
         self.C.gemm_set_ring_tn(self.RING_TN)
         self.C.gemm_set_ring_fill(self.RING_FILL)
         self.C.gemm_set_ring_m96(self.RING_M96)
+        self.C.gemm_set_d256_slots(self.D256_SLOTS)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))
@@ -251,7 +261,25 @@ class HipBackend(Backend):
         return (M > cls.SK_MAX_M or M > cls.TILED_ALL_M
                 or (M > cls.TILED_MIN_M and N >= cls.TILED_MIN_N))
 
+    def _d256_bn(self, M: int, N: int, K: int) -> int:
+        """Tile columns when this GEMM runs on gemm_d256_kernel, else 0
+        (mirrors d256_bn() in gemm.hip)."""
+        if not self.D256 or not (128 < M <= 256) or K % 64 or N > 32768 or not self._tiled(M, N):
+            return 0
+        return 128 if self.D256 == 128 and N % 128 == 0 else 64
+
+    @staticmethod
+    def _d256_kind(bn: int) -> int:  # lsd_gemm launch kind of gemm_d256
+        return 3 if bn == 128 else 2
+
+    def _d256_splits(self, N: int, K: int, bn: int, target: int) -> int:
+        tiles = math.ceil(N / bn)
+        return max(1, min(round(target / tiles), K // 64 // 2 or 1, 16))
+
     def _resid_splits(self, M: int, N: int, K: int) -> int:
+        bn = self._d256_bn(M, N, K)
+        if bn and self.D256_RESID:
+            return self._d256_splits(N, K, bn, self.D256_RESID_TARGET)
         if self._tiled(M, N):
             if M <= self.SK_MAX_M and self.TILED3_MAX and self.RING_TN in (0, 32, 64):
                 # decode rows on the 128x64 ring: as many splits as keep the
@@ -295,6 +323,9 @@ class HipBackend(Backend):
         return max(1, min(math.ceil(target / tiles), K // 32 // self.SK_MIN_STEPS or 1))
 
     def _gemm_kw(self, M: int, N: int, K: int, nw: int = 1):
+        bn = self._d256_bn(M, N, K)
+        if bn:
+            return self._d256_kind(bn), self._d256_splits(N, K, bn, self.D256_TARGET)
         if self._tiled(M, N):
             return True, 1
         return False, self._sk_splits(M, N, K, nw)
@@ -414,6 +445,9 @@ class HipBackend(Backend):
             return
         splits = self._resid_splits(M, N, K)
         tiled = self._tiled(M, N)
+        bn = self._d256_bn(M, N, K) if self.D256_RESID else 0
+        if bn:
+            tiled = self._d256_kind(bn)
         # decode split-K: hand the S partial slabs to the next norm (which
         # reads the rows anyway) instead of a last-arriver reduce in the GEMM
         defer = self.DEFER_RESID and not tiled and splits > 1

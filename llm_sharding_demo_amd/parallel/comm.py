@@ -75,11 +75,20 @@ class Transport:
     rank: int = 0
     world: int = 1
 
-    def send(self, t: torch.Tensor, dst: int, edge: str) -> SendHandle:
+    GRAPH_IO = False  # send / recv may not be captured into a hipGraph
+
+    def send(self, t: torch.Tensor, dst: int, edge: str, lane: int = 0) -> SendHandle:
         raise NotImplementedError
 
-    def irecv(self, out: torch.Tensor, src: int, edge: str) -> Handle:
+    def irecv(self, out: torch.Tensor, src: int, edge: str, lane: int = 0) -> Handle:
         raise NotImplementedError
+
+    def check_async(self) -> Optional[str]:
+        """Asynchronous data-plane error, if the backend reports any."""
+        return None
+
+    def abort(self) -> None:
+        """Unblock anything waiting on the data plane (native RCCL only)."""
 
     def broadcast_object(self, obj, src: int = 0):
         raise NotImplementedError
@@ -135,6 +144,11 @@ class _DistTransport(Transport):
 
     def _backend(self) -> str:
         raise NotImplementedError
+
+    @property
+    def num_comms(self) -> int:
+        """Data-plane communicators this rank belongs to (one per edge group)."""
+        return sum(1 for name in self.groups if self.grank in self._members(name))
 
     def _g(self, stage: int) -> int:
         return self.replica * self.P + stage
@@ -207,13 +221,13 @@ class NcclTransport(_DistTransport):
     def _backend(self) -> str:
         return "nccl"
 
-    def send(self, t, dst, edge):
+    def send(self, t, dst, edge, lane=0):
         g = self._edge_group(edge, self.rank, dst)
         if not t.is_contiguous():  # p2p needs a dense buffer (views of padded rows)
             t = t.contiguous()
         return SendHandle(self.dist.isend(t, self._g(dst), group=g))
 
-    def irecv(self, out, src, edge):
+    def irecv(self, out, src, edge, lane=0):
         g = self._edge_group(edge, src, self.rank)
         if out.is_contiguous():
             return Handle(out, self.dist.irecv(out, self._g(src), group=g))
@@ -227,12 +241,12 @@ class GlooTransport(_DistTransport):
     def _backend(self) -> str:
         return "gloo"
 
-    def send(self, t, dst, edge):
+    def send(self, t, dst, edge, lane=0):
         g = self._edge_group(edge, self.rank, dst)
         host = t.detach().to("cpu", copy=True) if t.device.type != "cpu" else t.detach().clone()
         return SendHandle(self.dist.isend(host, self._g(dst), group=g))
 
-    def irecv(self, out, src, edge):
+    def irecv(self, out, src, edge, lane=0):
         g = self._edge_group(edge, src, self.rank)
         if out.device.type == "cpu":
             return Handle(out, self.dist.irecv(out, self._g(src), group=g))
@@ -241,110 +255,147 @@ class GlooTransport(_DistTransport):
         return Handle(out, work, post=lambda: out.copy_(host))
 
 
-class _EventWork:
-    """torch-Work-like wait(): the caller's stream waits on a HIP event."""
-
-    def __init__(self, ev):
-        self.ev = ev
-
-    def wait(self) -> None:
-        torch.cuda.current_stream().wait_event(self.ev)
-
-
 class RcclTransport(_DistTransport):
-    """Pipeline edges on the native RCCL communicator (csrc/comm.cpp).
+    """Pipeline edges on the native RCCL communicator (csrc/comm.cpp), with
+    the decode step's receive and send captured INSIDE the stage's hipGraph.
 
-    Every edge (stage i -> i+1, and the token return P-1 -> 0) is its own
-    2-rank RCCL communicator with a dedicated comm stream. That stream keeps
-    the edge's operations in issue order on both ranks: the same ordering
-    ProcessGroupNCCL enforces, without which concurrent lanes could
-    interleave differently on the two GPUs.
+    Communicators: one 2-rank RCCL communicator per (pipeline edge, lane) --
+    edge = stage i -> i+1 or the token return P-1 -> 0, lane = the HIP stream
+    a microbatch group runs on (group g -> lane g % L on every stage,
+    parallel/pipeline.py).  RCCL requires the operations of a communicator to
+    execute in the same order on both ranks; a lane stream executes its items
+    in plan order on every rank, so each communicator's ops are totally
+    ordered without a dedicated comm stream or any event hop.
 
-    A send or receive is made device-async by three event waits:
-    - the comm stream waits for the caller's stream, so the data or buffer
-      is ready;
-    - ncclSend / ncclRecv run on the comm stream;
-    - the caller's stream waits on the completion event in `.wait()`.
-    No host sync is involved.
+    Ops are enqueued on the CURRENT stream: eagerly (the lane stream) or
+    during a graph capture (the capture stream -> replayed on the lane).  A
+    decode item therefore costs one graph launch: recv -> blocks -> send
+    (stage 0: embed -> blocks -> send, after its eager token-return recv;
+    stage P-1: recv -> blocks -> lm_head -> sampler -> send).  Sends and
+    receives return already-"complete" handles: every later use of the
+    buffers is on the same lane stream, so stream order is the
+    synchronisation.
 
-    The unique id of each edge is made by its first member and broadcast
-    over the gloo control group. Members then join in a fixed global order
-    (fwd0, fwd1, ..., ret), so the blocking inits complete left to right,
-    as in `warmup`."""
+    Failure handling: `check_async()` polls every communicator's
+    asynchronous error (ncclCommGetAsyncError); `abort()` aborts them all
+    (ncclCommAbort), which makes an RCCL kernel blocked on a dead or stalled
+    peer return, so the host threads waiting on the lanes wake up and the
+    engine fails its requests instead of hanging (runtime/scheduler.py
+    Watchdog).
+
+    Bring-up: the unique id of each communicator is made by its first member
+    and broadcast over the gloo control group; members join in a fixed global
+    order (edge-major, then lane), so the blocking inits complete left to
+    right, as in `warmup`."""
 
     EDGE_GROUPS = False
+    GRAPH_IO = True  # the pipeline may capture send / recv into decode graphs
 
     def _backend(self) -> str:
         return "gloo"  # control plane only; the data plane is native
 
-    def __init__(self, num_stages: int, replicas: int = 1):
+    def __init__(self, num_stages: int, replicas: int = 1, lanes: int = 2):
         super().__init__(num_stages, replicas)
         from ..ops.hip import _load
 
         self.C = _load()
-        self.comms: Dict[str, tuple] = {}  # edge -> (comm handle, comm stream, my index)
+        self.L = max(1, lanes)
+        self.comms: Dict[tuple, tuple] = {}  # (edge group name, lane) -> (handle, my index)
+        self.aborted = False
+        self._lock = threading.Lock()
         for name in self.groups:
             members = self._members(name)
-            uid = self.C.rccl_unique_id() if self.grank == members[0] else None
-            uid = self.broadcast_object(uid, src=members[0])
-            if self.grank in members:
-                me = members.index(self.grank)
-                h = self.C.rccl_comm_init(2, me, uid)
-                self.comms[name] = (h, torch.cuda.Stream(), me)
+            for lane in range(self.L):
+                uid = self.C.rccl_unique_id() if self.grank == members[0] else None
+                uid = self.broadcast_object(uid, src=members[0])
+                if self.grank in members:
+                    me = members.index(self.grank)
+                    self.comms[(name, lane)] = (self.C.rccl_comm_init(2, me, uid), me)
 
-    def _edge(self, edge: str, src: int, dst: int):
+    @property
+    def num_comms(self) -> int:
+        return len(self.comms)
+
+    def _edge(self, edge: str, src: int, dst: int, lane: int):
         name = f"r{self.replica}fwd{min(src, dst)}" if edge == "fwd" else f"r{self.replica}ret"
-        return self.comms[name]
+        if self.aborted:
+            raise TransportError(f"RCCL communicators aborted; {edge} edge unusable")
+        return self.comms[(name, lane % self.L)]
 
-    def send(self, t, dst, edge):
-        h, cs, me = self._edge(edge, self.rank, dst)
+    def send(self, t, dst, edge, lane: int = 0):
+        h, me = self._edge(edge, self.rank, dst, lane)
         if not t.is_contiguous():
             t = t.contiguous()
-        cs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(cs):
-            self.C.rccl_send(h, t, 1 - me)
-            ev = torch.cuda.Event()
-            ev.record(cs)
-        t.record_stream(cs)
-        return SendHandle(_EventWork(ev))
+        self.C.rccl_send(h, t, 1 - me)
+        t.record_stream(torch.cuda.current_stream())
+        return SendHandle()
 
-    def irecv(self, out, src, edge):
-        h, cs, me = self._edge(edge, src, self.rank)
-        buf = out if out.is_contiguous() else torch.empty(out.shape, dtype=out.dtype, device=out.device)
-        cs.wait_stream(torch.cuda.current_stream())  # the buffer's previous readers
-        with torch.cuda.stream(cs):
-            self.C.rccl_recv(h, buf, 1 - me)
-            ev = torch.cuda.Event()
-            ev.record(cs)
-        buf.record_stream(cs)
-        post = None if buf is out else (lambda: out.copy_(buf))
-        return Handle(out, _EventWork(ev), post=post)
+    def irecv(self, out, src, edge, lane: int = 0):
+        h, me = self._edge(edge, src, self.rank, lane)
+        if out.is_contiguous():
+            self.C.rccl_recv(h, out, 1 - me)
+            return Handle(out)
+        buf = torch.empty(out.shape, dtype=out.dtype, device=out.device)
+        self.C.rccl_recv(h, buf, 1 - me)
+        return Handle(out, post=lambda: out.copy_(buf))
+
+    # graph capture: the same enqueue on the capture stream
+    capture_send = send
+    capture_recv = irecv
 
     def warmup(self, device) -> None:
-        """One exchange per edge, in the global edge order (checks the data)."""
-        for name, (h, cs, me) in self.comms.items():
+        """One exchange per communicator, in the global order (checks the data)."""
+        for (name, lane), (h, me) in self.comms.items():
             src = self._members(name)[0]
-            buf = torch.full((4,), float(src), device=device)
+            kind = "ret" if name.endswith("ret") else "fwd"
             if me == 0:
-                self.send(buf, self._stage_of(self._members(name)[1]),
-                          "ret" if name.endswith("ret") else "fwd").wait()
+                buf = torch.full((4,), float(src * self.L + lane), device=device)
+                self.send(buf, self._stage_of(self._members(name)[1]), kind, lane)
+                torch.cuda.synchronize(device)
             else:
                 got = torch.zeros(4, device=device)
-                self.irecv(got, self._stage_of(src), "ret" if name.endswith("ret") else "fwd").wait()
+                self.irecv(got, self._stage_of(src), kind, lane).wait()
                 torch.cuda.synchronize(device)
-                if float(got[0].item()) != float(src):
-                    raise TransportError(f"warmup RCCL p2p on {name}: got {got[0].item()}, want {src}")
+                if float(got[0].item()) != float(src * self.L + lane):
+                    raise TransportError(f"warmup RCCL p2p on {name}/lane{lane}: got {got[0].item()}")
         torch.cuda.synchronize(device)
         self.barrier()
 
     def _stage_of(self, grank: int) -> int:
         return grank % self.P
 
+    def check_async(self) -> Optional[str]:
+        """First asynchronous RCCL error of any communicator, or None."""
+        with self._lock:
+            if self.aborted:
+                return None
+            for (name, lane), (h, _) in self.comms.items():
+                e = self.C.rccl_async_error(h)
+                if e not in (0, 7):  # ncclSuccess, ncclInProgress
+                    return f"RCCL {name}/lane{lane}: {self.C.rccl_error_string(e)}"
+        return None
+
+    def abort(self) -> None:
+        """Abort every communicator (unblocks kernels waiting on a peer)."""
+        with self._lock:
+            if self.aborted:
+                return
+            self.aborted = True
+            for h, _ in self.comms.values():
+                try:
+                    self.C.rccl_comm_abort(h)
+                except RuntimeError:
+                    pass
+
     def close(self) -> None:
-        torch.cuda.synchronize()
-        for h, _, _ in self.comms.values():
-            self.C.rccl_comm_destroy(h)
-        self.comms.clear()
+        with self._lock:
+            if self.aborted:
+                self.comms.clear()
+                return
+            torch.cuda.synchronize()
+            for h, _ in self.comms.values():
+                self.C.rccl_comm_destroy(h)
+            self.comms.clear()
 
 
 # ---------------------------------------------------------------------------
@@ -465,7 +516,7 @@ class LoopbackTransport(Transport):
     def __init__(self, fabric: LocalFabric, rank: int):
         self.fabric, self.rank, self.world = fabric, rank, fabric.P
 
-    def send(self, t, dst, edge):
+    def send(self, t, dst, edge, lane=0):
         key = (edge, self.rank, dst)
         cur = torch.cuda.current_stream(t.device)
         buf = t.detach().clone()  # enqueued on the sender's stream
@@ -474,7 +525,7 @@ class LoopbackTransport(Transport):
         self.fabric.q(key).put((buf, ev))
         return SendHandle()
 
-    def irecv(self, out, src, edge):
+    def irecv(self, out, src, edge, lane=0):
         key = (edge, src, self.rank)
         fabric = self.fabric
 
@@ -501,7 +552,7 @@ class LocalTransport(Transport):
     def __init__(self, fabric: LocalFabric, rank: int):
         self.fabric, self.rank, self.world = fabric, rank, fabric.P
 
-    def send(self, t, dst, edge):
+    def send(self, t, dst, edge, lane=0):
         key = (edge, self.rank, dst)
         seq = self.fabric.next_seq(key)
         payload = t.detach().clone()
@@ -517,7 +568,7 @@ class LocalTransport(Transport):
         self.fabric.q(key).put(payload)
         return SendHandle()
 
-    def irecv(self, out, src, edge):
+    def irecv(self, out, src, edge, lane=0):
         key = (edge, src, self.rank)
         fabric = self.fabric
 
@@ -566,8 +617,10 @@ def init_distributed(backend: str, device_type: str, timeout_s: float = 600.0) -
 
 
 def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1) -> Transport:
-    if kind == "rccl":  # native communicator (csrc/comm.cpp)
-        t = RcclTransport(num_stages, replicas)
+    if kind == "rccl":  # native communicator (csrc/comm.cpp), one per (edge, lane)
+        import os
+
+        t = RcclTransport(num_stages, replicas, lanes=int(os.environ.get("LSD_LANES", "2")))
         t.warmup(device)
         return t
     if kind == "nccl":

@@ -267,6 +267,14 @@ class StageWorker:
         self.step_events: List[tuple] = []   # stage 0: (step, event) at each step start
         self.readout = None        # stage 0: callable(step, plan, ret_tensor) for token readout
         self._tls = threading.local()
+        # Decode graphs that contain their own edge receive and send (native
+        # RCCL transport, parallel/comm.py RcclTransport): a decode item is
+        # then ONE graph launch per stage.  Items carrying prefill chunks keep
+        # eager transfers (their sizes vary), as does stage 0's token-return
+        # receive (the host reads it back and may re-gather the rows).
+        self.graph_io = bool(transport is not None and getattr(transport, "GRAPH_IO", False)
+                             and self.device.type == "cuda"
+                             and os.environ.get("LSD_GRAPH_IO", "1") != "0")
 
     # ------------------------------------------------------------------
     def configure(self, groups: int, cap: int) -> None:
@@ -276,6 +284,14 @@ class StageWorker:
         self.groups = {g: GroupState(self, g, cap) for g in range(groups)}
         self.send_pending.clear()
         self.recv.clear()
+
+    def lane_of(self, g: int) -> int:
+        return g % max(1, len(self.lanes))
+
+    def _io(self, gp: GroupPlan) -> bool:
+        """Does this item's decode graph carry its own receive / send?"""
+        return (self.graph_io and self.use_graphs and gp.kind != "fwd_b" and gp.b > 0
+                and not gp.chunks and self.P > 1)
 
     def on_lane(self, g: int):
         if not self.lanes:
@@ -372,7 +388,7 @@ class StageWorker:
         T = gp.prefill_tokens
         if T > 0:
             out.append(("fwd", self.r - 1, self._hp(gs, T)))
-        if gp.b > 0:
+        if gp.b > 0 and not self._io(gp):
             out.append(("fwd", self.r - 1, gs.hd[: gp.b]))
         return out
 
@@ -395,7 +411,8 @@ class StageWorker:
             # receive behind it (stream-level wait, no host sync)
             for h in self.send_pending.pop(gp.g, []):
                 h.wait()
-            self.recv[(gp.g, id(gp))] = [self.t.irecv(buf, src, edge) for edge, src, buf in tg]
+            lane = self.lane_of(gp.g)
+            self.recv[(gp.g, id(gp))] = [self.t.irecv(buf, src, edge, lane) for edge, src, buf in tg]
 
     def _take_recv(self, gp: GroupPlan) -> List[torch.Tensor]:
         hs = self.recv.pop((gp.g, id(gp)), None)
@@ -418,6 +435,10 @@ class StageWorker:
         # other buffers (overlap); otherwise after
         early = (nx is not None and nx.g != gp.g
                  and not (self._buffers(self._recv_targets(nx)) & self._buffers(self._recv_targets(gp))))
+        if early and self.graph_io and self.lane_of(nx.g) == self.lane_of(gp.g):
+            # in-stream transfers: a receive queued on this lane ahead of the
+            # current item would hold its compute until the peer's data lands
+            early = False
         if early:
             self._post(nx)
         # outputs of this group's previous item must have left before we overwrite them
@@ -459,11 +480,14 @@ class StageWorker:
                 finals = x
             elif x is not None:
                 sends.append(x)
-        # --- decode rows (hipGraph per (bucket, context bucket))
+        # --- decode rows (hipGraph per (bucket, context bucket)); with graph
+        # I/O the graph receives its input and sends its output itself
+        io = self._io(gp)
+        lane = self.lane_of(gp.g)
         if gp.b > 0:
-            inp = gs.tin[: gp.b] if self.first else ins[k]
-            out = self._decode(gp, gs, inp)
-            if not self.last:
+            inp = gs.tin[: gp.b] if self.first else (gs.hd[: gp.b] if io else ins[k])
+            out = self._decode(gp, gs, inp, io)
+            if not self.last and not io:
                 sends.append(out)
         if self.last:
             J = gp.n_final
@@ -471,11 +495,11 @@ class StageWorker:
             if J:
                 gs.ensure_tokret(self, nret)
                 gs.tokret[gp.b: nret].copy_(finals)
-            if nret and self.P > 1:
-                self.send_pending.setdefault(gp.g, []).append(self.t.send(gs.tokret[:nret], 0, "ret"))
+            if nret and self.P > 1 and not io:
+                self.send_pending.setdefault(gp.g, []).append(self.t.send(gs.tokret[:nret], 0, "ret", lane))
         else:
             for x in sends:
-                self.send_pending.setdefault(gp.g, []).append(self.t.send(x, self.r + 1, "fwd"))
+                self.send_pending.setdefault(gp.g, []).append(self.t.send(x, self.r + 1, "fwd", lane))
 
     def _apply_rows(self, gp: GroupPlan, gs: GroupState) -> None:
         """New composition: rows [0, n) from the plan, pad rows [n, b) idle on
@@ -530,17 +554,24 @@ class StageWorker:
                              [c.greedy for c in fc], [c.seed for c in fc], dev)
         return be.sample(logits, samp, st.cfg.vocab_size)
 
-    def _decode(self, gp: GroupPlan, gs: GroupState, inp: torch.Tensor) -> torch.Tensor:
-        key = (gp.b, gp.ctxb)
+    def _decode(self, gp: GroupPlan, gs: GroupState, inp: torch.Tensor, io: bool = False) -> torch.Tensor:
+        key = (gp.b, gp.ctxb, io)
+        lane = self.lane_of(gp.g)
 
         def body():
+            if io and not self.first:  # the edge receive, inside the graph
+                self.t.capture_recv(inp, self.r - 1, "fwd", lane)
             meta = gs.meta(gp.b, gp.ctxb)
             out = self.stage.forward(meta, inp, head=True, variant=gp.g & 1)
             meta.advance()
             if not self.last:
+                if io:
+                    self.t.capture_send(out, self.r + 1, "fwd", lane)
                 return out
             samp = gs.samp(gp.b)
             self.stage.backend.sample_into(out, samp, self.stage.cfg.vocab_size, gs.tokret[: gp.b])
+            if io:
+                self.t.capture_send(gs.tokret[: gp.b], 0, "ret", lane)
             return gs.tokret[: gp.b]
 
         graphs = self.use_graphs and self.device.type == "cuda"
@@ -567,13 +598,14 @@ class StageWorker:
         T = gp.fwd_rows
         meta = BatchMeta.build([self.compat_slot], [0], [T], self.device)
         x = ins[0]
+        lane = self.lane_of(gp.g)
         if self.last:
             # only the real vocabulary crosses (the HIP lm_head pads it)
             out = st.forward(meta, x, all_logits=True)[:, : st.cfg.vocab_size].contiguous()
-            self.send_pending.setdefault(gp.g, []).append(self.t.send(out, 0, "ret"))
+            self.send_pending.setdefault(gp.g, []).append(self.t.send(out, 0, "ret", lane))
         else:
             out = st.forward(meta, x)
-            self.send_pending.setdefault(gp.g, []).append(self.t.send(out, self.r + 1, "fwd"))
+            self.send_pending.setdefault(gp.g, []).append(self.t.send(out, self.r + 1, "fwd", lane))
 
     # ------------------------------------------------------------------
     def _capture(self, fn):

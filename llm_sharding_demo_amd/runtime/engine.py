@@ -171,6 +171,13 @@ class Engine:
                 self.workers[0].readout = self._ship_readout
         else:
             raise ValueError(f"unknown mode {mode!r}")
+        # dist mode: every rank watches its own progress and data plane (a
+        # follower stuck behind a dead peer aborts its communicators too)
+        self.watchdog = None
+        if mode == "dist" and cfg.round_timeout_s > 0:
+            from .scheduler import Watchdog
+
+            self.watchdog = Watchdog(self, cfg.round_timeout_s)
         # one KV-slot pool per pipeline replica (the scheduler allocates for all)
         self.slot_pools = [_make_slot_allocator(self.kv_slots) for _ in range(self.R)]
         self.slots = self.slot_pools[0]
@@ -445,14 +452,20 @@ class Engine:
                 worker.start_stats()
                 started = True
             nxt = recv()
+            self.round_started = time.monotonic()  # watchdog: host blocked inside a step
             worker.run_step(cur, nxt if not nxt.stop else None)
+            self.round_started = None
+            if not self.healthy:
+                raise RuntimeError(self.last_error)
             cur = nxt
 
     def _follower_stats(self, worker: StageWorker, end_plan: StepPlan) -> None:
         if not end_plan.timing:
             worker.stats = None
             return
+        self.round_started = time.monotonic()
         worker.sync()
+        self.round_started = None
         st = worker.end_stats()
         if self.mode == "local":
             self._stats_q.put(st)
@@ -586,6 +599,8 @@ class Engine:
         if self.rank == 0:
             for t in self._tok_threads:
                 t.join(timeout=30)
+        if self.watchdog is not None:
+            self.watchdog.close()
         self.transport.close()  # native RCCL communicators (no-op for torch groups)
         self.transport.barrier()
         if dist.is_initialized():

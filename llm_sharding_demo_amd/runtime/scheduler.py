@@ -608,7 +608,13 @@ class Scheduler:
 
 
 class Watchdog:
-    """Marks the engine unhealthy when the pipeline stops making progress."""
+    """Marks the engine unhealthy when the pipeline stops making progress or
+    the data plane reports an asynchronous error, and then aborts the data
+    plane: with the native RCCL transport a kernel waiting on a dead or
+    stalled peer would otherwise spin forever (and every host thread waiting
+    on its stream with it); ncclCommAbort makes it return, the waits drain
+    and the requests fail instead of hanging (the reference
+    fails a request after its 30 s HTTP timeout, server.py:173-174)."""
 
     def __init__(self, engine, round_timeout_s: float, poll_s: float = 0.25):
         self.engine = engine
@@ -621,16 +627,35 @@ class Watchdog:
 
     def _loop(self) -> None:
         while not self._stop.wait(self.poll):
+            if self.fired:
+                continue
+            tr = getattr(self.engine, "transport", None)
+            try:
+                err = tr.check_async() if tr is not None else None
+            except Exception as e:  # noqa: BLE001 - a broken communicator is an error too
+                err = f"{type(e).__name__}: {e}"
+            if err:
+                self._fire("DataPlaneError", err)
+                continue
             started = getattr(self.engine, "round_started", None)
-            if started is None or self.fired:
+            if started is None:
                 continue
             elapsed = time.monotonic() - started
             if elapsed > self.timeout:
-                self.fired = True
-                msg = f"no pipeline progress for {elapsed:.0f} s (deadline {self.timeout:.0f} s)"
-                log.error("watchdog: %s; marking engine unhealthy", msg)
-                self.engine.healthy = False
-                self.engine.last_error = f"WatchdogTimeout: {msg}"
+                self._fire("WatchdogTimeout",
+                           f"no pipeline progress for {elapsed:.0f} s (deadline {self.timeout:.0f} s)")
+
+    def _fire(self, kind: str, msg: str) -> None:
+        self.fired = True
+        log.error("watchdog: %s: %s; marking engine unhealthy and aborting the data plane", kind, msg)
+        self.engine.healthy = False
+        self.engine.last_error = f"{kind}: {msg}"
+        tr = getattr(self.engine, "transport", None)
+        if tr is not None:
+            try:
+                tr.abort()
+            except Exception as e:  # noqa: BLE001
+                log.error("watchdog: data-plane abort failed: %s", e)
 
     def close(self) -> None:
         self._stop.set()

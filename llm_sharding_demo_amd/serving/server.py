@@ -105,7 +105,8 @@ def create_app(cfg: EngineConfig, engine=None, shard: Optional[ShardRunner] = No
         from ..runtime.scheduler import Watchdog
 
         engine.start_loop()
-        watchdog = Watchdog(engine, cfg.round_timeout_s)
+        # dist engines run their own (every rank); local ones get one here
+        watchdog = getattr(engine, "watchdog", None) or Watchdog(engine, cfg.round_timeout_s)
     app.state.watchdog = watchdog
 
     def _role_is(*roles):

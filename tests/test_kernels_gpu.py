@@ -235,6 +235,53 @@ def test_ring_gemm_96_row_tiles(C, CNT, M, K):
         C.gemm_set_ring_tn(128)
 
 
+@pytest.fixture(params=[(2, 3), (3, 3), (2, 2), (2, 4), (3, 2)])
+def D256(C, request):
+    """(launch kind, ring slots) of the 8-wave all-rows kernel gemm_d256:
+    kind 2 = 64-column tiles, 3 = 128-column tiles."""
+    kind, slots = request.param
+    C.gemm_set_d256_slots(slots)
+    yield C, kind
+    C.gemm_set_d256_slots(3)
+
+
+@pytest.mark.parametrize("M", [1, 100, 129, 200, 256])
+@pytest.mark.parametrize("K,splits", [(64, 1), (192, 1), (192, 3), (640, 2), (640, 5), (1600, 3), (1600, 1)])
+def test_d256_gemm_epilogues(D256, CNT, M, K, splits):
+    """256-row decode kernel: every epilogue, row tails (1 to 256 rows), a
+    partial last column tile, 1 to 25 k-steps (fewer than, equal to and more
+    than the ring), split-K with the in-kernel last-arriver combine and the
+    residual slabs folded by the norm; repeated launches reuse the re-armed
+    ticket counters."""
+    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
+
+    C, kind = D256
+    N = 384 if kind == 3 else 352  # 352: a partial last 64-wide tile
+    a, w, bias = bf(M, K, seed=80), bf(N, K, scale=0.05, seed=81), bf(N, scale=0.1, seed=82)
+    y_ref = ref.linear(a, w, bias)
+    for _ in range(2):
+        close(C.linear(a, w, bias, 0, kind, splits, CNT), y_ref, 3e-2)
+    close(C.linear(a, w, bias, 1, kind, splits, CNT), ref.gelu_new(y_ref), 3e-2)
+    w2 = w[:256].contiguous()
+    y = C.linear(a, interleave_gate_up(w2, 128).contiguous(), None, 2, kind, splits, CNT)
+    close(y, ref.silu_mul(*ref.linear(a, w2).split(128, 1)), 3e-2)
+    close(C.linear_f32(a, w, kind, splits, CNT), ref.linear(a, w), 2e-3, 1e-3)
+    x = torch.randn(M, N, device=DEV)
+    x_ref = x + y_ref
+    slab = C.linear_residual(a, w, bias, x, splits, kind, CNT, False)
+    if splits > 1:
+        assert slab is not None and slab.shape == (splits, M, N)
+        C.norm(x, slab, bias, None, None, 0.0, True, None, False)
+    else:
+        assert slab is None
+    close(x, x_ref, 2e-3, 1e-3)
+    # split-K combine order is fixed: bit-identical on a second launch
+    if splits > 1:
+        assert torch.equal(C.linear(a, w, bias, 0, kind, splits, CNT),
+                           C.linear(a, w, bias, 0, kind, splits, CNT))
+    assert int(CNT.abs().sum()) == 0  # every ticket re-armed
+
+
 @pytest.fixture
 def BIG(C):
     """Force the pipelined 256x256 kernel for every tiled launch with M >= 256."""
@@ -300,16 +347,19 @@ def _cache(slots, n_kv, S, hd):
 
 
 @pytest.mark.parametrize("rope", [False, True])
-@pytest.mark.parametrize("mode", ["decode1", "decode4", "tiled", "big"])
+@pytest.mark.parametrize("mode", ["decode1", "decode4", "tiled", "big", "d256", "d256s3"])
 def test_qkv_kv_append(C, CNT, rope, mode):
     from llm_sharding_demo_amd.ops.hip import rope_pair_permutation, rope_table
 
     nh, n_kv, hd, H = 4, 2, 64, 256
     qs, kvs = nh * hd, n_kv * hd
-    tiled = mode in ("tiled", "big")
-    splits = 4 if mode == "decode4" else 1
-    # decode: 10 tokens of 2 sequences; tiled: 2 sequences of 150 tokens
-    n0, n1 = (4, 6) if not tiled else (150, 150)
+    tiled = mode in ("tiled", "big", "d256", "d256s3")
+    splits = 4 if mode == "decode4" else (3 if mode == "d256s3" else 1)
+    # decode: 10 tokens of 2 sequences; tiled: 2 sequences of 150 tokens;
+    # d256: 200 decode-like rows (100 + 100) on the 256-row kernel (kind 2)
+    n0, n1 = (4, 6) if not tiled else ((100, 100) if mode.startswith("d256") else (150, 150))
+    if mode.startswith("d256"):
+        tiled = 2
     T, slots, S = n0 + n1, 3, 320
     a, w, bias = bf(T, H, seed=13), bf(qs + 2 * kvs, H, scale=0.05, seed=14), bf(qs + 2 * kvs, scale=0.1, seed=15)
     tslot = torch.tensor([0] * n0 + [2] * n1, dtype=torch.int32, device=DEV)

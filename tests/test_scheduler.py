@@ -177,3 +177,43 @@ def test_metrics_throughput_is_wall_clock():
         m.observe_request(10, time.monotonic() - t0)
     tps = m.tokens_per_second()
     assert 120 < tps < 220, tps  # ~40 tokens / 0.2 s, not 40 / 0.8 s
+
+
+def test_watchdog_aborts_data_plane_on_async_error_and_timeout():
+    """The watchdog fires on a data-plane async error (polled every tick) and
+    on a stalled round, marks the engine unhealthy and aborts the transport
+    (the native RCCL transport's abort unblocks kernels waiting on a dead
+    peer; tests/test_comm_abort_gpu.py covers that half on the GPU)."""
+    import time
+    from types import SimpleNamespace
+
+    from llm_sharding_demo_amd.runtime.scheduler import Watchdog
+
+    class FakeTransport:
+        def __init__(self, err=None):
+            self.err, self.aborts = err, 0
+
+        def check_async(self):
+            return self.err
+
+        def abort(self):
+            self.aborts += 1
+
+    tr = FakeTransport("RCCL r0fwd0/lane1: remote process exited")
+    eng = SimpleNamespace(transport=tr, healthy=True, last_error=None, round_started=None)
+    wd = Watchdog(eng, round_timeout_s=60, poll_s=0.02)
+    deadline = time.monotonic() + 5
+    while eng.healthy and time.monotonic() < deadline:
+        time.sleep(0.02)
+    wd.close()
+    assert not eng.healthy and eng.last_error.startswith("DataPlaneError") and tr.aborts == 1
+
+    tr2 = FakeTransport()
+    eng2 = SimpleNamespace(transport=tr2, healthy=True, last_error=None,
+                           round_started=time.monotonic())
+    wd2 = Watchdog(eng2, round_timeout_s=0.2, poll_s=0.02)
+    deadline = time.monotonic() + 5
+    while eng2.healthy and time.monotonic() < deadline:
+        time.sleep(0.02)
+    wd2.close()
+    assert not eng2.healthy and eng2.last_error.startswith("WatchdogTimeout") and tr2.aborts == 1
