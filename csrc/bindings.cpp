@@ -600,5 +600,28 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // decode GEMM column tile 128 (NW = 2) above this many rows
   m.def("gemm_set_nw2_rows", [](int64_t v) { lsd_gemm_set_nw2_rows((int)v); });
   m.def("gemm_sk_nw", [](int64_t M, int64_t epi) { return lsd_gemm_sk_nw((int)M, (int)epi); });
+  // A HIP stream whose kernels may only run on the CUs set in `mask` (32-bit
+  // words; bit i = CU i of the device's mask numbering) -- spatial
+  // partitioning of the chip between microbatch lanes (parallel/pipeline.py
+  // LSD_LANE_CU_MASK).  Returns the raw hipStream_t for torch.cuda.ExternalStream;
+  // the stream lives until the process exits.
+  m.def("stream_with_cu_mask", [](std::vector<int64_t> mask) {
+    std::vector<uint32_t> m32(mask.begin(), mask.end());
+    hipStream_t s = nullptr;
+    check_hip(hipExtStreamCreateWithCUMask(&s, (uint32_t)m32.size(), m32.data()), "hipExtStreamCreateWithCUMask");
+    return reinterpret_cast<int64_t>(s);
+  });
+  m.def("stream_cu_mask", [](int64_t stream, int64_t words) {
+    std::vector<uint32_t> m32((size_t)words, 0u);
+    check_hip(hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), (uint32_t)words, m32.data()),
+              "hipExtStreamGetCUMask");
+    return std::vector<int64_t>(m32.begin(), m32.end());
+  });
+  m.def("device_cu_count", []() {
+    int dev = 0, n = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    check_hip(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+    return n;
+  });
   m.attr("arch") = "gfx950";
 }

@@ -236,6 +236,11 @@ class EngineConfig:
     # auto | nccl | gloo | local | http | loopback (P stage threads on one GPU,
     # device-async event hand-off: single-GPU rehearsal of the RCCL schedule)
     transport: str = "auto"
+    # Boundary hidden states on the wire: "fp32" (the residual stream as is:
+    # bit-identical to one stage) or "bf16" (half the bytes per hop; the
+    # stream is rounded to bf16 at each stage boundary).  The reference ships
+    # them as JSON floats (server.py:140,148).
+    wire_dtype: str = "fp32"
     # Serving (runtime/scheduler.py): concurrent /generate requests arriving
     # within batch_window_ms share one pipeline round; a round running longer
     # than round_timeout_s marks the engine unhealthy; an HTTP request waits at
@@ -278,6 +283,7 @@ class EngineConfig:
             dtype=_env("DTYPE", "bf16"),
             weights=os.environ.get("WEIGHTS") or None,
             transport=_env("TRANSPORT", "auto"),
+            wire_dtype=_env("WIRE_DTYPE", "fp32"),
             dp_replicas=int(_env("DP_REPLICAS", "1") or 1),
             batch_window_ms=float(_env("BATCH_WINDOW_MS", "2.0")),
             prefill_chunk=int(_env("PREFILL_CHUNK", "0")),

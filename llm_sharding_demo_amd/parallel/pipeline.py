@@ -158,6 +158,14 @@ class GroupState:
         self._metas: Dict[tuple, BatchMeta] = {}
         self.rows_n = 0
 
+    def wire_buf(self, w: "StageWorker", b: int) -> Optional[torch.Tensor]:
+        """Persistent wire-dtype staging rows of the decode receive (graph I/O)."""
+        if w.wire is None or w.first:
+            return None
+        if getattr(self, "_wire", None) is None:
+            self._wire = torch.empty(self.cap, w.H, dtype=w.wire, device=w.device)
+        return self._wire[:b]
+
     def ensure_tokret(self, w: "StageWorker", n: int) -> None:
         """Grow the token-return vector to >= n entries (prefill finals ride
         behind the decode rows).  Growing drops the captured graphs that
@@ -238,8 +246,12 @@ class StepStats:
 
 class StageWorker:
     def __init__(self, stage: StageModel, transport: Optional[Transport], stage_idx: int,
-                 num_stages: int, scratch_slot: int = 0, compat_slot: int = 0):
+                 num_stages: int, scratch_slot: int = 0, compat_slot: int = 0,
+                 wire: Optional[torch.dtype] = None):
         self.stage = stage
+        # hidden states on the forward edge in this dtype (None: as computed,
+        # fp32); converted right before the send / right after the receive
+        self.wire = wire
         self.t = transport
         self.r = stage_idx
         self.P = num_stages
@@ -257,6 +269,13 @@ class StageWorker:
         n_lanes = int(os.environ.get("LSD_LANES", "2"))
         self.lanes = ([torch.cuda.Stream(self.device) for _ in range(n_lanes)]
                       if self.device.type == "cuda" else [])
+        # LSD_LANE_CU_MASK: give each lane its own share of the CUs (spatial
+        # partition) instead of letting the lanes' kernels interleave on all
+        # of them -- "split" (contiguous halves of the mask numbering) or
+        # "interleave" (every n_lanes-th CU)
+        cu_mode = os.environ.get("LSD_LANE_CU_MASK", "")
+        if cu_mode and self.lanes and n_lanes > 1:
+            self.lanes = _cu_masked_lanes(self.device, n_lanes, cu_mode)
         self.groups: Dict[int, GroupState] = {}
         self.cap = 1
         self.send_pending: Dict[int, List[SendHandle]] = {}
@@ -412,7 +431,30 @@ class StageWorker:
             for h in self.send_pending.pop(gp.g, []):
                 h.wait()
             lane = self.lane_of(gp.g)
-            self.recv[(gp.g, id(gp))] = [self.t.irecv(buf, src, edge, lane) for edge, src, buf in tg]
+            self.recv[(gp.g, id(gp))] = [self._recv(buf, src, edge, lane) for edge, src, buf in tg]
+
+    # wire dtype (C-CODEC): hidden states cross the forward edge as self.wire
+    def _recv(self, buf: torch.Tensor, src: int, edge: str, lane: int, stage=None,
+              capture: bool = False):
+        if self.wire is None or edge != "fwd" or buf.dtype == self.wire:
+            return (self.t.capture_recv if capture else self.t.irecv)(buf, src, edge, lane)
+        if stage is None:
+            stage = torch.empty(buf.shape, dtype=self.wire, device=buf.device)
+        if capture:  # inside the graph: receive, then widen in place
+            self.t.capture_recv(stage, src, edge, lane)
+            buf.copy_(stage)
+            return None
+        inner = self.t.irecv(stage, src, edge, lane)
+
+        def post():
+            inner.wait()
+            buf.copy_(stage)
+        return Handle(buf, post=post)
+
+    def _send(self, x: torch.Tensor, dst: int, edge: str, lane: int, capture: bool = False):
+        if self.wire is not None and edge == "fwd" and x.dtype != self.wire:
+            x = x.to(self.wire)
+        return (self.t.capture_send if capture else self.t.send)(x, dst, edge, lane)
 
     def _take_recv(self, gp: GroupPlan) -> List[torch.Tensor]:
         hs = self.recv.pop((gp.g, id(gp)), None)
@@ -496,10 +538,10 @@ class StageWorker:
                 gs.ensure_tokret(self, nret)
                 gs.tokret[gp.b: nret].copy_(finals)
             if nret and self.P > 1 and not io:
-                self.send_pending.setdefault(gp.g, []).append(self.t.send(gs.tokret[:nret], 0, "ret", lane))
+                self.send_pending.setdefault(gp.g, []).append(self._send(gs.tokret[:nret], 0, "ret", lane))
         else:
             for x in sends:
-                self.send_pending.setdefault(gp.g, []).append(self.t.send(x, self.r + 1, "fwd", lane))
+                self.send_pending.setdefault(gp.g, []).append(self._send(x, self.r + 1, "fwd", lane))
 
     def _apply_rows(self, gp: GroupPlan, gs: GroupState) -> None:
         """New composition: rows [0, n) from the plan, pad rows [n, b) idle on
@@ -560,18 +602,18 @@ class StageWorker:
 
         def body():
             if io and not self.first:  # the edge receive, inside the graph
-                self.t.capture_recv(inp, self.r - 1, "fwd", lane)
+                self._recv(inp, self.r - 1, "fwd", lane, stage=gs.wire_buf(self, gp.b), capture=True)
             meta = gs.meta(gp.b, gp.ctxb)
             out = self.stage.forward(meta, inp, head=True, variant=gp.g & 1)
             meta.advance()
             if not self.last:
                 if io:
-                    self.t.capture_send(out, self.r + 1, "fwd", lane)
+                    self._send(out, self.r + 1, "fwd", lane, capture=True)
                 return out
             samp = gs.samp(gp.b)
             self.stage.backend.sample_into(out, samp, self.stage.cfg.vocab_size, gs.tokret[: gp.b])
             if io:
-                self.t.capture_send(gs.tokret[: gp.b], 0, "ret", lane)
+                self._send(gs.tokret[: gp.b], 0, "ret", lane, capture=True)
             return gs.tokret[: gp.b]
 
         graphs = self.use_graphs and self.device.type == "cuda"
@@ -602,10 +644,10 @@ class StageWorker:
         if self.last:
             # only the real vocabulary crosses (the HIP lm_head pads it)
             out = st.forward(meta, x, all_logits=True)[:, : st.cfg.vocab_size].contiguous()
-            self.send_pending.setdefault(gp.g, []).append(self.t.send(out, 0, "ret", lane))
+            self.send_pending.setdefault(gp.g, []).append(self._send(out, 0, "ret", lane))
         else:
             out = st.forward(meta, x)
-            self.send_pending.setdefault(gp.g, []).append(self.t.send(out, self.r + 1, "fwd", lane))
+            self.send_pending.setdefault(gp.g, []).append(self._send(out, self.r + 1, "fwd", lane))
 
     # ------------------------------------------------------------------
     def _capture(self, fn):
@@ -667,6 +709,23 @@ class StageWorker:
         finally:
             self._tls.shared.__exit__(None, None, None)
             self._tls.shared = None
+
+
+def _cu_masked_lanes(dev: torch.device, n: int, mode: str) -> List[torch.cuda.ExternalStream]:
+    from ..ops.hip import _load
+
+    C = _load()
+    with torch.cuda.device(dev):
+        cus = C.device_cu_count()
+        words = (cus + 31) // 32
+        lanes = []
+        for l in range(n):
+            bits = [c for c in range(cus) if ((c % n == l) if mode == "interleave" else (c * n // cus == l))]
+            mask = [0] * words
+            for c in bits:
+                mask[c // 32] |= 1 << (c % 32)
+            lanes.append(torch.cuda.ExternalStream(C.stream_with_cu_mask(mask), device=dev))
+    return lanes
 
 
 def _h2d(vals, dtype, dev) -> torch.Tensor:

@@ -246,8 +246,11 @@ class Engine:
                           variants=[p[i] for p in self.unit_plans] if self.unit_plans else None)
 
     def _worker(self, st: StageModel, t, i: int) -> StageWorker:
+        if self.cfg.wire_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"wire_dtype must be fp32 or bf16, got {self.cfg.wire_dtype!r}")
         return StageWorker(st, t, i, self.P, scratch_slot=self.kv_slots,
-                           compat_slot=self.kv_slots + 1)
+                           compat_slot=self.kv_slots + 1,
+                           wire=torch.bfloat16 if self.cfg.wire_dtype == "bf16" else None)
 
     @property
     def is_coordinator(self) -> bool:
@@ -654,7 +657,7 @@ class Engine:
                 self.plan_ch.send(r, StepPlan(step=-1, end=True))
             dev = self.devices[0]
             x = h.to(dev).contiguous()
-            self.transport.send(x, 1, "fwd").wait()
+            w0._send(x, 1, "fwd", 0).wait()  # in the wire dtype stage 1 expects
             out = torch.empty(T, self.mcfg.vocab_size, dtype=torch.float32, device=dev)
             self.transport.irecv(out, self.P - 1, "ret").wait()
             if dev.type == "cuda":
