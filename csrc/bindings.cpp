@@ -50,6 +50,10 @@ hipError_t lsd_attn_prefill(const bf16* q, long ldq, const bf16* kc, const bf16*
                             const int* tiles, int n_tiles, const int* seq_slots,
                             const int* q_start, const int* cu_q, bf16* out, long ldo, int nh,
                             int n_kv, int hd, int max_seq, float scale_log2, hipStream_t st);
+hipError_t lsd_attn_oproj(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
+                          const int* seq_slots, const int* qpos, int B, int nh, int n_kv, int hd,
+                          int max_seq, float scale_log2, const bf16* W, long ldw, const bf16* bias,
+                          float* x, int N, int NC, float* part, int* cnt, hipStream_t st);
 int lsd_gemv_ok(int M, int K, int epi, int norm);
 void lsd_gemv_set_nt(int v);
 hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st);
@@ -476,6 +480,43 @@ torch::Tensor attn_decode(torch::Tensor q, torch::Tensor kc, torch::Tensor vc,
   return out;
 }
 
+// x[B, N] += bias + attention(q, cache) @ w^T in ONE launch (B <= 4 decode
+// rows): the fused attention + output projection + residual kernel.
+void attn_oproj(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor seq_slots,
+                torch::Tensor qpos, int64_t nh, torch::Tensor w, c10::optional<torch::Tensor> bias,
+                torch::Tensor x, int64_t nc, torch::Tensor counters) {
+  need(q, torch::kBFloat16, "q");
+  need_rows(q, "q");
+  check_cache(kc, vc);
+  const int B = q.size(0), n_kv = kc.size(1), hd = kc.size(3);
+  TORCH_CHECK(B >= 1 && B <= 4, "attn_oproj: 1 <= B <= 4 rows, got ", B);
+  TORCH_CHECK(q.size(1) == nh * hd && nh % n_kv == 0, "q must be [B, nh*hd]");
+  TORCH_CHECK(hd == 64 || hd == 128, "head_dim must be 64 or 128");
+  const int G = nh / n_kv;
+  TORCH_CHECK((hd == 64 && G == 1) || (hd == 128 && (G == 1 || G == 2 || G == 4 || G == 8)),
+              "attn_oproj: unsupported head_dim / GQA group (", hd, ", ", G, ")");
+  need(seq_slots, torch::kInt32, "seq_slots");
+  need(qpos, torch::kInt32, "qpos");
+  TORCH_CHECK(seq_slots.numel() == B && qpos.numel() == B, "seq_slots/qpos [B]");
+  need(w, torch::kBFloat16, "w");
+  need_rows(w, "w");
+  TORCH_CHECK(w.size(1) == nh * hd, "w must be [N, nh*hd]");
+  const int N = w.size(0);
+  need(x, torch::kFloat32, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(0) == B && x.size(1) == N, "x must be contiguous [B, N]");
+  TORCH_CHECK(nc >= 1 && nc <= N, "column chunk in [1, N]");
+  const int C = (N + nc - 1) / nc;
+  need(counters, torch::kInt32, "counters");
+  TORCH_CHECK(counters.is_contiguous() && counters.numel() >= C, "counter buffer too small");
+  auto part = torch::empty({(long)C * n_kv * B * nc}, x.options());
+  const float sl2 = 1.4426950408889634f / std::sqrt((float)hd);
+  check_hip(lsd_attn_oproj(bptr(q), q.stride(0), bptr(kc), bptr(vc), seq_slots.data_ptr<int>(),
+                           qpos.data_ptr<int>(), B, nh, n_kv, hd, kc.size(2), sl2, bptr(w), w.stride(0),
+                           opt_bias(bias, N), x.data_ptr<float>(), N, (int)nc, part.data_ptr<float>(),
+                           counters.data_ptr<int>(), cur_stream()),
+            "attn_oproj");
+}
+
 torch::Tensor attn_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc,
                            torch::Tensor tiles, torch::Tensor seq_slots, torch::Tensor q_start,
                            torch::Tensor cu_q, int64_t nh) {
@@ -563,6 +604,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm", &norm);
   m.def("attn_decode", &attn_decode);
   m.def("attn_prefill", &attn_prefill);
+  m.def("attn_oproj", &attn_oproj);
   m.def("sample", &sample);
   m.def("sample_into", &sample_into);
   m.def("gemv", &gemv);

@@ -199,6 +199,203 @@ __global__ __launch_bounds__(NWV * 64) void attn_decode_kernel(
   }
 }
 
+// Decode attention FUSED with the attention output projection and its
+// residual add, for small batches (single stream: B <= 4 rows).  At batch 1
+// a GPT-2 XL layer's attention (5.7 us) and out-projection GEMV (4.8 us, a
+// 5 MB weight read at 1.1 TB/s) are both latency-bound launches
+// (profiles/r2_single_stream_analysis.log); here one launch does both:
+//   block (kv head h, column chunk c): attention of every sequence for the G
+//   query heads of kv head h (the decode kernel's loop, K and V requested in
+//   one round; recomputed by each of the C chunk blocks of h -- L2-served
+//   re-reads of a few tens of KB), kept in fp32 in LDS; then the partial
+//   out-projection  part[c][h][b][n] = sum_{k in head h's slice} o[b][k] W[n][k]
+//   for the chunk's NC output columns (W's [N][nh*HD] rows: the slice is
+//   G*HD contiguous bf16 per column).
+// The n_kv partials of a column chunk are summed by the chunk's LAST-arriving
+// block in kv-head order (deterministic), plus the bias, into the fp32
+// residual x.  Hand-off (guide §6 Guideline 16 / MI355X_MICROARCH hand-off
+// table row 1): write-through (sc1, relaxed agent-scope) partial stores ->
+// every wave's vmcnt(0) -> barrier -> one lane's agent-scope ticket add; the
+// block whose add returns n_kv - 1 reads the partials with sc1 loads.
+template <int HD, int G, int NWV, int BMAX>
+__global__ __launch_bounds__(NWV * 64) void attn_oproj_kernel(
+    const bf16* __restrict__ q, long ldq, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const int* __restrict__ seq_slots, const int* __restrict__ qpos, int B, int n_kv, int max_seq,
+    float scale_log2, const bf16* __restrict__ W, long ldw, const bf16* __restrict__ bias, float* x,
+    int N, int NC, float* part, int* cnt) {
+  constexpr int LPK = HD / 8;    // lanes per key row
+  constexpr int KPI = 64 / LPK;  // keys per wave-instruction
+  constexpr int U = 2;
+  constexpr int KS = G * HD;     // this kv head's slice of the out-projection's K
+  constexpr int LPC = KS / 8 <= 64 ? KS / 8 : 64;  // lanes per output column
+  constexpr int R = KS / (8 * LPC);                 // 16-B pieces of W per lane
+  constexpr int CPI = 64 / LPC;                     // columns per wave-instruction
+  static_assert(64 % LPC == 0 && R * 8 * LPC == KS, "out-projection slice per lane");
+  __shared__ float sm[NWV][G][LPK][10];
+  __shared__ float so[BMAX][KS];
+  __shared__ int s_flag;
+  const int kvh = blockIdx.x, c = blockIdx.y;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int ds = lane % LPK, kg = lane / LPK;
+
+  for (int b = 0; b < B; ++b) {
+    const int ctx = qpos[b] + 1;
+    const long base = ((long)seq_slots[b] * n_kv + kvh) * (long)max_seq * HD + ds * 8;
+    float qf[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const bf16x8 qq = ld8(q + (long)b * ldq + (long)(kvh * G + g) * HD + ds * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[g][j] = bf2f(qq[j]) * scale_log2;
+    }
+    float m[G], l[G], o[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      m[g] = NEG;
+      l[g] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
+    }
+    for (int c0 = w * KPI; c0 < ctx; c0 += NWV * KPI * U) {
+      bf16x8 kv[U], vv[U];
+      int key[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // K and V of the round requested together
+        key[u] = c0 + u * NWV * KPI + kg;
+        const int kk = min(key[u], ctx - 1);
+        kv[u] = ld8(kc + base + (long)kk * HD);
+        vv[u] = ld8(vc + base + (long)kk * HD);
+      }
+      float sc[G][U];
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float acc = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc += qf[g][j] * bf2f(kv[u][j]);
+#pragma unroll
+          for (int msk = 1; msk < LPK; msk <<= 1) acc += wave_xchg_n(acc, msk);
+          sc[g][u] = key[u] < ctx ? acc : NEG;
+        }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float mx = sc[g][0];
+#pragma unroll
+        for (int u = 1; u < U; ++u) mx = fmaxf(mx, sc[g][u]);
+        const float mn = fmaxf(m[g], mx);
+        const float alpha = exp2f(m[g] - mn);
+        float p[U], ps = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          p[u] = exp2f(sc[g][u] - mn);
+          ps += p[u];
+        }
+        l[g] = l[g] * alpha + ps;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float a = o[g][j] * alpha;
+#pragma unroll
+          for (int u = 0; u < U; ++u) a += p[u] * bf2f(vv[u][j]);
+          o[g][j] = a;
+        }
+        m[g] = mn;
+      }
+    }
+#pragma unroll
+    for (int msk = LPK; msk < 64; msk <<= 1) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float mo = wave_xor_n(m[g], msk), lo = wave_xor_n(l[g], msk);
+        const float mn = fmaxf(m[g], mo);
+        const float a = exp2f(m[g] - mn), bb = exp2f(mo - mn);
+        l[g] = l[g] * a + lo * bb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[g][j] = o[g][j] * a + wave_xor_n(o[g][j], msk) * bb;
+        m[g] = mn;
+      }
+    }
+    if (kg == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        sm[w][g][ds][0] = m[g];
+        sm[w][g][ds][1] = l[g];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sm[w][g][ds][2 + j] = o[g][j];
+      }
+    }
+    __syncthreads();
+    if (w == 0 && kg == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float mm = NEG;
+#pragma unroll
+        for (int ww = 0; ww < NWV; ++ww) mm = fmaxf(mm, sm[ww][g][ds][0]);
+        float ll = 0.f, oo[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ww = 0; ww < NWV; ++ww) {
+          const float f = exp2f(sm[ww][g][ds][0] - mm);
+          ll += sm[ww][g][ds][1] * f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) oo[j] += sm[ww][g][ds][2 + j] * f;
+        }
+        const float inv = ll > 0.f ? 1.f / ll : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) so[b][g * HD + ds * 8 + j] = oo[j] * inv;
+      }
+    }
+    __syncthreads();  // so[b] complete; sm reused by the next sequence
+  }
+
+  // ---- partial out-projection of this kv head's slice, NC columns
+  const int n0 = c * NC;
+  const int sub = lane % LPC;
+  for (int cb = w * CPI; cb < NC; cb += NWV * CPI) {  // wave-uniform trip count (lane reductions)
+    const int cc = cb + lane / LPC, n = n0 + cc;
+    const bool valid = cc < NC && n < N;
+    float wf[R][8];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+      const bf16x8 wv = ld8(W + (long)min(n, N - 1) * ldw + (long)kvh * KS + (rr * LPC + sub) * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wf[rr][j] = bf2f(wv[j]);
+    }
+    for (int b = 0; b < B; ++b) {
+      float acc = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += so[b][(rr * LPC + sub) * 8 + j] * wf[rr][j];
+#pragma unroll
+      for (int msk = 1; msk < LPC; msk <<= 1) acc += wave_xchg_n(acc, msk);
+      if (valid && sub == 0)
+        __hip_atomic_store(part + (((long)c * n_kv + kvh) * B + b) * NC + cc, acc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(cnt + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_flag = (t == n_kv - 1);
+    if (t == n_kv - 1) __hip_atomic_store(cnt + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_flag) return;
+  // ---- last arriver: x[b][n] += bias[n] + sum_h part[c][h][b][n], kv heads in order
+  for (int i = threadIdx.x; i < B * NC; i += NWV * 64) {
+    const int b = i / NC, cc = i % NC, n = n0 + cc;
+    if (n >= N) continue;
+    float s = 0.f;
+#pragma unroll 8
+    for (int h = 0; h < n_kv; ++h)
+      s += __hip_atomic_load(part + (((long)c * n_kv + h) * B + b) * NC + cc, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    float* xp = x + (long)b * N + n;
+    *xp = *xp + (s + (bias ? bf2f(bias[n]) : 0.f));
+  }
+}
+
 // Merge split-K decode partials: one block per (sequence, head).
 template <int HD>
 __global__ __launch_bounds__(64) void attn_decode_combine_kernel(const float* part_o,
@@ -632,4 +829,32 @@ extern "C" hipError_t lsd_attn_prefill(const bf16* q, long ldq, const bf16* kc, 
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+// Fused decode attention + output projection + residual add (B <= 4).
+// part: fp32 [C][n_kv][B][NC] workspace, cnt: >= C zeroed ticket counters
+// (re-armed by each chunk's last arriver).
+extern "C" hipError_t lsd_attn_oproj(const bf16* q, long ldq, const bf16* kc, const bf16* vc,
+                                     const int* seq_slots, const int* qpos, int B, int nh, int n_kv,
+                                     int hd, int max_seq, float scale_log2, const bf16* W, long ldw,
+                                     const bf16* bias, float* x, int N, int NC, float* part, int* cnt,
+                                     hipStream_t st) {
+  if (B == 0) return hipSuccess;
+  if (B > 4 || NC < 1) return hipErrorInvalidValue;
+  const int G = nh / n_kv;
+  const dim3 grid(n_kv, (N + NC - 1) / NC), block(512);
+#define LSD_AOP(HDV, GV)                                                                           \
+  if (hd == HDV && G == GV) {                                                                      \
+    hipLaunchKernelGGL((attn_oproj_kernel<HDV, GV, 8, 4>), grid, block, 0, st, q, ldq, kc, vc,     \
+                       seq_slots, qpos, B, n_kv, max_seq, scale_log2, W, ldw, bias, x, N, NC, part, \
+                       cnt);                                                                       \
+    return hipGetLastError();                                                                      \
+  }
+  LSD_AOP(64, 1)
+  LSD_AOP(128, 1)
+  LSD_AOP(128, 2)
+  LSD_AOP(128, 4)
+  LSD_AOP(128, 8)
+#undef LSD_AOP
+  return hipErrorInvalidValue;
 }

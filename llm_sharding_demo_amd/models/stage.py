@@ -93,8 +93,17 @@ class StageModel:
         xn = be.layernorm(r, w(i, "ln_1.weight"), w(i, "ln_1.bias"), c.norm_eps)
         q = be.qkv_kv_append(xn, w(i, "attn.c_attn.weight"), w(i, "attn.c_attn.bias"),
                              self.kv.k(li), self.kv.v(li), meta, c)
+        self._attn_out(q, li, meta, w(i, "attn.c_proj.weight"), w(i, "attn.c_proj.bias"), r)
+
+    def _attn_out(self, q, li: int, meta: BatchMeta, wo, bo, r: Residual) -> None:
+        """Attention + output projection + residual add: one fused launch when
+        the backend has it for this shape (small decode batches), else two."""
+        be = self.backend
+        fused = getattr(be, "attention_oproj", None)
+        if fused is not None and fused(q, self.kv.k(li), self.kv.v(li), meta, wo, bo, r):
+            return
         o = be.attention(q, self.kv.k(li), self.kv.v(li), meta)
-        be.linear_residual(o, w(i, "attn.c_proj.weight"), w(i, "attn.c_proj.bias"), r)
+        be.linear_residual(o, wo, bo, r)
 
     def _gpt2_mlp(self, i: int, r: Residual) -> None:
         be, c, w = self.backend, self.cfg, self._lw
@@ -107,8 +116,7 @@ class StageModel:
         xn = be.rmsnorm(r, w(i, "input_layernorm.weight"), c.norm_eps)
         q = be.qkv_kv_append(xn, w(i, "self_attn.qkv.weight"), None,
                              self.kv.k(li), self.kv.v(li), meta, c)
-        o = be.attention(q, self.kv.k(li), self.kv.v(li), meta)
-        be.linear_residual(o, w(i, "self_attn.o_proj.weight"), None, r)
+        self._attn_out(q, li, meta, w(i, "self_attn.o_proj.weight"), None, r)
 
     def _llama_mlp(self, i: int, r: Residual) -> None:
         be, c, w = self.backend, self.cfg, self._lw

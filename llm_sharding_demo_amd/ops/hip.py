@@ -181,10 +181,16 @@ class HipBackend(Backend):
     RESID_LONGK_MIN_M = int(os.environ.get("LSD_RESID_LONGK_MIN_M", "128"))
     TILED_MIN_M = int(os.environ.get("LSD_TILED_MIN_M", "64"))
     # Decode GEMMs of 129-256 rows on the 8-wave all-rows kernel (gemm.hip
-    # gemm_d256_kernel): tile columns (64 / 128, 0 = off, the 128x64 ring),
-    # ring depth, and the workgroup targets that set the K splits of the
-    # in-kernel-combined GEMMs (QKV, MLP-up) and of the residual slabs
-    D256 = int(os.environ.get("LSD_D256", "0"))
+    # gemm_d256_kernel): 1 = auto (long-K GEMMs, below), 64 / 128 = every
+    # 129-256-row tiled GEMM with that tile width (A/B), 0 = off (the 128x64
+    # ring).  Ring depth, and the workgroup targets that set the K splits of
+    # the in-kernel-combined GEMMs (QKV, MLP-up) and of the residual slabs.
+    # Auto (tools/bench_d256.py at 256 rows, profiles/r3_d256_ab.log): Llama-3
+    # 8B gate/up 84.6 -> 69.0 us (128-wide tiles, 224 workgroups, no split),
+    # QKV 35.6 -> 31.9 (64-wide, 2 K splits); GPT-2 XL's K = 1600 GEMMs stay on
+    # the ring (16.6 vs 16.9-20.6 us; bench 49.0k vs 45.2-47.1k tok/s)
+    D256 = int(os.environ.get("LSD_D256", "1"))
+    D256_MIN_K = int(os.environ.get("LSD_D256_MIN_K", "4096"))
     D256_SLOTS = int(os.environ.get("LSD_D256_SLOTS", "3"))
     D256_TARGET = int(os.environ.get("LSD_D256_TARGET", "192"))
     D256_RESID_TARGET = int(os.environ.get("LSD_D256_RESID_TARGET", "192"))
@@ -266,6 +272,10 @@ class HipBackend(Backend):
         (mirrors d256_bn() in gemm.hip)."""
         if not self.D256 or not (128 < M <= 256) or K % 64 or N > 32768 or not self._tiled(M, N):
             return 0
+        if self.D256 == 1:  # auto: long-K GEMMs only; 128-wide tiles when they alone fill the chip
+            if K < self.D256_MIN_K:
+                return 0
+            return 128 if N % 128 == 0 and N // 128 >= 128 else 64
         return 128 if self.D256 == 128 and N % 128 == 0 else 64
 
     @staticmethod
@@ -424,6 +434,35 @@ class HipBackend(Backend):
             meta._tiles = tiles
         return self.C.attn_prefill(q, cache_k, cache_v, tiles, meta.seq_slots, meta.q_start,
                                    meta.cu_q, nh)
+
+    # Decode attention fused with the output projection + residual add at
+    # <= ATTN_OPROJ_MAX_M rows (attention.hip attn_oproj_kernel): one launch
+    # instead of attention + out-projection GEMV.  Off by default: the
+    # cross-block hand-off of the per-head partials (write-through stores,
+    # ticket, last-arriver reload) costs more than the kernel boundary it
+    # removes -- single stream GPT-2 XL 1.385 -> 1.570 ms, small 0.290 ->
+    # 0.316, Llama-3 8B 3.19 -> 3.37 (profiles/r3_attn_oproj_single_stream.log)
+    ATTN_OPROJ_MAX_M = int(os.environ.get("LSD_ATTN_OPROJ_MAX_M", "0"))
+
+    def attention_oproj(self, q, cache_k, cache_v, meta, w, b, r: Residual) -> bool:
+        """x += attention(q) @ w^T + b in one kernel; False = not applicable
+        (the caller runs attention + linear_residual)."""
+        M = q.shape[0]
+        if not meta.is_decode or M > min(self.ATTN_OPROJ_MAX_M, 4) or M < 1:
+            return False
+        n_kv, hd = cache_k.shape[1], cache_k.shape[3]
+        nh = q.shape[1] // hd
+        G = nh // n_kv
+        if not ((hd == 64 and G == 1) or (hd == 128 and G in (1, 2, 4, 8))):
+            return False
+        if r.pending:
+            self.flush(r)
+        N = w.shape[0]
+        C = max(1, -(-256 // n_kv))           # ~256 blocks: n_kv heads x C column chunks
+        nc = -(-(-(-N // C)) // 16) * 16      # chunk columns, a multiple of 16
+        self.C.attn_oproj(q, cache_k, cache_v, meta.seq_slots, meta.token_pos, nh, w, b, r.x, nc,
+                          self.counters)
+        return True
 
     def linear(self, a, w, b=None, act: str = "none"):
         code = _EPI[act]

@@ -619,3 +619,40 @@ def test_sampler_small_vocab(C, V, Vp):
                      counter_uniform(seeds.cpu(), step.cpu()), V)
     assert out.cpu().tolist() == exp.tolist()
     assert all(0 <= t < V for t in out.cpu().tolist())
+
+
+@pytest.mark.parametrize("hd,nh,n_kv,N", [(64, 25, 25, 1600), (64, 12, 12, 768), (128, 32, 8, 4096),
+                                          (128, 8, 2, 320), (128, 16, 2, 256), (128, 8, 8, 1024)])
+@pytest.mark.parametrize("B", [1, 2, 4])
+@pytest.mark.parametrize("nc", [16, 160, 0])
+def test_attention_oproj_fused(C, CNT, hd, nh, n_kv, N, B, nc):
+    """Fused decode attention + output projection + residual add (small
+    batches): x += attention(q) @ W^T + b, against the fp32 reference of the
+    two separate ops; column chunks of 16 / 160 / the engine's choice (0),
+    contexts 1..300, deterministic across launches (fixed kv-head order)."""
+    from llm_sharding_demo_amd.ops.hip import HipBackend  # noqa: F401
+
+    slots, S = 6, 300
+    kc, vc = bf(slots, n_kv, S, hd, seed=96), bf(slots, n_kv, S, hd, seed=97)
+    q = bf(B, nh * hd, seed=98)
+    w, bias = bf(N, nh * hd, scale=0.03, seed=99), bf(N, scale=0.1, seed=100)
+    g = torch.Generator().manual_seed(B + N)
+    seq_slots = torch.randperm(slots, generator=g)[:B].int().to(DEV)
+    pos = torch.tensor([0, 299, 17, 150][:B], dtype=torch.int32, device=DEV)
+    if nc == 0:
+        C_ = max(1, -(-256 // n_kv))
+        nc = -(-(-(-N // C_)) // 16) * 16
+    cu = torch.arange(B + 1, dtype=torch.int32)
+    o_ref = ref.attention(q.reshape(B, nh, hd).cpu(), kc.cpu(), vc.cpu(), seq_slots.cpu(), pos.cpu(), cu)
+    y_ref = o_ref.reshape(B, nh * hd).float() @ w.float().cpu().t() + bias.float().cpu()
+    x0 = torch.randn(B, N, device=DEV)
+    x = x0.clone()
+    C.attn_oproj(q, kc, vc, seq_slots, pos, nh, w, bias, x, nc, CNT)
+    close(x - x0, y_ref, 2e-2)
+    x2 = x0.clone()
+    C.attn_oproj(q, kc, vc, seq_slots, pos, nh, w, bias, x2, nc, CNT)
+    assert torch.equal(x, x2)
+    x3 = x0.clone()
+    C.attn_oproj(q, kc, vc, seq_slots, pos, nh, w, None, x3, nc, CNT)  # no bias
+    close(x3 - x0, y_ref - bias.float().cpu(), 2e-2)
+    assert int(CNT.abs().sum()) == 0
