@@ -27,6 +27,8 @@ void lsd_gemm_set_ring_tn(int v);
 void lsd_gemm_set_ring_fill(int v);
 void lsd_gemm_set_ring_m96(int v);
 void lsd_gemm_set_d256_slots(int v);
+void lsd_gemm_set_ring8(int v);
+void lsd_gemm_set_ring8_slots(int v);
 int lsd_gemm_d256_bn(int kind, int M, int N, int K);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
@@ -626,6 +628,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_ring_m96", [](int64_t v) { lsd_gemm_set_ring_m96((int)v); });
   // gemm_d256 (launch kind 2 / 3: all <= 256 rows in one tile, 64 / 128 columns): ring depth
   m.def("gemm_set_d256_slots", [](int64_t v) { lsd_gemm_set_d256_slots((int)v); });
+  m.def("gemm_set_ring8", [](int64_t v) { lsd_gemm_set_ring8((int)v); });
+  m.def("gemm_set_ring8_slots", [](int64_t v) { lsd_gemm_set_ring8_slots((int)v); });
   m.def("gemm_d256_bn", [](int64_t kind, int64_t M, int64_t N, int64_t K) {
     return lsd_gemm_d256_bn((int)kind, (int)M, (int)N, (int)K);
   });

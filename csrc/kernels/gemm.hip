@@ -532,29 +532,13 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk)
   return *reinterpret_cast<const bf16x8*>(tile + row * 128 + pch * 16);
 }
 
-// Epilogue through LDS (free after the main loop's last barrier): the MFMA C
-// layout gives each lane 4 rows x 1 column, i.e. 2-4-byte scattered stores;
-// transposing the 128x128 fp32 tile through LDS turns every global store
-// into a 16-byte row-contiguous vector (256 B per 16 lanes).
-// TN = tile columns (128, or 64 for the narrow ring tiles); wave (wm, wn)
-// holds rows wm*64 + [0, 64) and columns wn*TN/2 + [0, TN/2).
-template <int EPI, int TN = TBN, int MI = 4>
-__device__ __forceinline__ void tiled_epilogue(const GemmParams& p, f32x4 (&acc)[MI][TN / 32], char* smem,
-                                               int m0, int n0, int split, int wm, int wn, int r,
-                                               int g) {
-  constexpr int CLD = TN + 4;  // bank skew
+// Store loop of an fp32 [TM][TN + 4] C tile in LDS: NT threads, one 8-column
+// row chunk each per pass, 16-byte global stores (epilogue8).
+template <int EPI, int TN, int TM, int NT>
+__device__ __forceinline__ void ct_store(const GemmParams& p, const float* ct, int m0, int n0, int split) {
+  constexpr int CLD = TN + 4;
   constexpr int CPR = TN / 8;  // 8-column chunks per row
-  constexpr int TM = 32 * MI;  // tile rows (wave rows of 16 * MI)
-  float* ct = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < TN / 32; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        ct[(wm * 16 * MI + i * 16 + 4 * g + q) * CLD + wn * (TN / 2) + j * 16 + r] = acc[i][j][q];
-  __syncthreads();
-  for (int c = threadIdx.x; c < TM * CPR; c += 256) {
+  for (int c = threadIdx.x; c < TM * CPR; c += NT) {
     const int row = c / CPR, n = n0 + (c % CPR) * 8, m = m0 + row;
     if (m >= p.M || n >= p.N) continue;
     const float* src = ct + row * CLD + (c % CPR) * 8;
@@ -577,6 +561,30 @@ __device__ __forceinline__ void tiled_epilogue(const GemmParams& p, f32x4 (&acc)
       epilogue8<EPI>(p, m, n, v, split);
     }
   }
+}
+
+// Epilogue through LDS (free after the main loop's last barrier): the MFMA C
+// layout gives each lane 4 rows x 1 column, i.e. 2-4-byte scattered stores;
+// transposing the 128x128 fp32 tile through LDS turns every global store
+// into a 16-byte row-contiguous vector (256 B per 16 lanes).
+// TN = tile columns (128, or 64 for the narrow ring tiles); wave (wm, wn)
+// holds rows wm*64 + [0, 64) and columns wn*TN/2 + [0, TN/2).
+template <int EPI, int TN = TBN, int MI = 4>
+__device__ __forceinline__ void tiled_epilogue(const GemmParams& p, f32x4 (&acc)[MI][TN / 32], char* smem,
+                                               int m0, int n0, int split, int wm, int wn, int r,
+                                               int g) {
+  constexpr int CLD = TN + 4;  // bank skew
+  constexpr int TM = 32 * MI;  // tile rows (wave rows of 16 * MI)
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < TN / 32; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        ct[(wm * 16 * MI + i * 16 + 4 * g + q) * CLD + wn * (TN / 2) + j * 16 + r] = acc[i][j][q];
+  __syncthreads();
+  ct_store<EPI, TN, TM, 256>(p, ct, m0, n0, split);
 }
 
 template <int EPI>
@@ -724,6 +732,126 @@ __global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_
   }
   __syncthreads();  // every wave's fragment reads retired before the C tile overwrites the slots
   tiled_epilogue<EPI, TN, MI>(p, acc, smem, m0, n0, split, wm, wn, r, g);
+}
+
+// Stage a [ROWS][64 k] tile (the lds_frag image) with NWAVES waves sharing
+// the ROWS / 8 wave-instructions; `wi` = this wave's index among them.
+template <int ROWS, int NWAVES>
+__device__ __forceinline__ void stage_rows(char* lds_tile, const bf16* src, long ld, int row0, int row_max,
+                                           int k0, int wi) {
+  const int lane = lane_id();
+  constexpr int PER_WAVE = ROWS / 8 / NWAVES;
+  static_assert(PER_WAVE * 8 * NWAVES == ROWS, "rows split evenly over the loading waves");
+#pragma unroll
+  for (int q = 0; q < PER_WAVE; ++q) {
+    const int inst = wi * PER_WAVE + q;
+    const int row = inst * 8 + (lane >> 3);
+    const int lch = (lane & 7) ^ ((row >> 1) & 7);
+    const bf16* gp = src + (long)min(row0 + row, row_max) * ld + k0 + lch * 8;
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)gp, (lds_void*)(lds_tile + inst * 1024), 16, 0, 0);
+  }
+}
+
+// 8-wave variant of the 128x64 decode ring (512 threads, same tiles, same
+// 3-slot ring, same grid).  In the 4-wave ring every wave issues its 6 LDS-DMA
+// instructions per k-step (each ~60-185 issue cycles beside MFMAs, microarch
+// 'LDS-DMA piece issue cost') in the same instruction stream as its 16 MFMAs,
+// so a step costs issue + MFMA + reads instead of their max.  Two layouts:
+//   VAR 1: waves 0-3 compute (64 x 32 each, as the 4-wave ring) and never touch
+//          VMEM; waves 4-7 are loaders (6 glds per step) -- one of each per SIMD;
+//   VAR 2: all 8 waves compute 32 x 32 and each issues 3 glds per step.
+// One raw s_barrier per k-step publishes step kt's slot (every loader waited
+// its own DMAs with a counted vmcnt) and proves step kt-1's slot free.
+template <int EPI, int VAR, int SLOTS>
+__global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int D = SLOTS - 1, TN = 64, TM = TBM;
+  constexpr int CW = VAR == 1 ? 4 : 8;           // computing waves
+  constexpr int LWN = VAR == 1 ? 4 : 8;          // loading waves
+  constexpr int MI = TM / 16 / (CW / 2);         // 16-row MFMA tiles per computing wave: 4 / 2
+  constexpr int JT = 2;                          // 16-column MFMA tiles per computing wave (32 cols)
+  constexpr int A_BYTES = TM * TBK * 2;
+  constexpr int SLOT_BYTES = A_BYTES + TN * TBK * 2;
+  constexpr int LPS = (TM + TN) / 8 / LWN;      // glds per loading wave per k-step: 6 / 3
+  constexpr int CLD = TN + 4;
+  constexpr int SMEM = SLOTS * SLOT_BYTES > TM * CLD * 4 ? SLOTS * SLOT_BYTES : TM * CLD * 4;
+  static_assert(VAR == 1 || VAR == 2, "ring8 layout");
+  static_assert(SLOTS >= 3 && SLOTS <= 5 && (SLOTS - 2) * LPS <= 63, "ring depth / vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];  // [slot][A|W]; then the C tile
+  const int nwg = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int per_split = tiles_m * tiles_n;
+  const int split = bid / per_split;
+  const int t = bid % per_split;
+  const int tm = t % tiles_m, tn = t / tiles_m;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int KT = p.K / TBK;
+  const int kb = (int)((long)KT * split / p.splits), ke = (int)((long)KT * (split + 1) / p.splits);
+
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const bool loader = VAR == 2 || w >= 4;
+  const bool compute = VAR == 2 || w < 4;
+  const int lw = VAR == 1 ? w - 4 : w;
+  const int wm = (w & (CW - 1)) >> 1, wn = w & 1;
+  const int r = lane & 15, g = lane >> 4;
+
+  f32x4 acc[MI][JT];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int kt, int slot) {
+    char* b = smem + slot * SLOT_BYTES;
+    stage_rows<TM, LWN>(b, p.A, p.lda, m0, p.M - 1, kt * TBK, lw);
+    stage_rows<TN, LWN>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, kt * TBK, lw);
+  };
+  if (loader) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (kb + d < ke) issue(kb + d, d);
+  }
+  int slot = 0;
+  for (int kt = kb; kt < ke; ++kt) {
+    if (loader) {  // this wave's DMAs of step kt landed; the later issued steps stay in flight
+      const int later = min(D - 1, ke - 1 - kt);
+      if (D >= 4 && later >= 3) __builtin_amdgcn_s_waitcnt(vmcnt_imm(3 * LPS));
+      else if (D >= 3 && later == 2) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * LPS));
+      else if (later == 1) __builtin_amdgcn_s_waitcnt(vmcnt_imm(LPS));
+      else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    }
+    __builtin_amdgcn_s_barrier();
+    if (loader && kt + D < ke) issue(kt + D, slot == 0 ? SLOTS - 1 : slot - 1);
+    if (compute) {
+      const char* ta = smem + slot * SLOT_BYTES;
+      const char* tw = ta + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[MI], wf[JT];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[i] = lds_frag(ta, wm * 16 * MI + i * 16 + r, kk * 4 + g);
+#pragma unroll
+        for (int j = 0; j < JT; ++j) wf[j] = lds_frag(tw, wn * 32 + j * 16 + r, kk * 4 + g);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < JT; ++j) acc[i][j] = mfma16(af[i], wf[j], acc[i][j]);
+      }
+    }
+    slot = slot == SLOTS - 1 ? 0 : slot + 1;
+  }
+  __syncthreads();  // fragment reads retired (and no DMA pending) before the C tile overwrites the slots
+  float* ct = reinterpret_cast<float*>(smem);
+  if (compute) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < JT; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          ct[(wm * 16 * MI + i * 16 + 4 * g + q) * CLD + wn * 32 + j * 16 + r] = acc[i][j][q];
+  }
+  __syncthreads();
+  ct_store<EPI, TN, TM, 512>(p, ct, m0, n0, split);
 }
 
 // ---------------------------------------------------------------------------
@@ -1413,6 +1541,9 @@ static int g_ring_slots = 3;  // lsd_gemm_set_ring_slots(): 3 or 4
 static int g_ring_tn = 128;   // lsd_gemm_set_ring_tn(): ring tile columns, 128, 64, 32 or 0 (auto 32/64)
 static int g_ring_fill = 128; // auto: 32-wide tiles below this many 64-wide workgroups
 static int g_ring_m96 = 0;    // lsd_gemm_set_ring_m96(): largest 96-row-tile ring grid (0 = off)
+// lsd_gemm_set_ring8(): 128x64 decode ring on 8 waves (gemm_ring8_kernel): 0 off, 1 loader waves, 2 all compute
+static int g_ring8 = 0;
+static int g_ring8_slots = 3;  // lsd_gemm_set_ring8_slots(): ring depth of layout 2 (3..5)
 static int g_d256_slots = 3;  // lsd_gemm_set_d256_slots(): gemm_d256 ring depth 2..4 (BN 128: at most 3)
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
@@ -1547,7 +1678,17 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
       }
     }
     if (tm * tn64 * p.splits <= g_tiled3_max_blocks) {
-      hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 64>), dim3(tm * tn64 * p.splits), dim3(256), 0, st, p, tm, tn64);
+      const dim3 g8(tm * tn64 * p.splits), b8(512);
+      if (g_ring8 == 1)
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 1, 3>), g8, b8, 0, st, p, tm, tn64);
+      else if (g_ring8 == 2 && g_ring8_slots == 4)
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 4>), g8, b8, 0, st, p, tm, tn64);
+      else if (g_ring8 == 2 && g_ring8_slots == 5)
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 5>), g8, b8, 0, st, p, tm, tn64);
+      else if (g_ring8 == 2)
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3>), g8, b8, 0, st, p, tm, tn64);
+      else
+        hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 64>), dim3(tm * tn64 * p.splits), dim3(256), 0, st, p, tm, tn64);
       return hipGetLastError();
     }
   }
@@ -1578,6 +1719,8 @@ extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; 
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }
 extern "C" void lsd_gemm_set_ring_fill(int v) { g_ring_fill = v; }
 extern "C" void lsd_gemm_set_ring_m96(int v) { g_ring_m96 = v; }
+extern "C" void lsd_gemm_set_ring8(int v) { g_ring8 = (v == 1 || v == 2) ? v : 0; }
+extern "C" void lsd_gemm_set_ring8_slots(int v) { g_ring8_slots = v < 3 ? 3 : (v > 5 ? 5 : v); }
 extern "C" void lsd_gemm_set_d256_slots(int v) { g_d256_slots = v < 2 ? 2 : (v > 4 ? 4 : v); }
 // columns per gemm_d256 tile of a launch of this kind (0: not a d256 launch):
 // the split workspace and ticket counters are sized from it (bindings.cpp)

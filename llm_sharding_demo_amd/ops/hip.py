@@ -196,6 +196,15 @@ class HipBackend(Backend):
     D256_RESID_TARGET = int(os.environ.get("LSD_D256_RESID_TARGET", "192"))
     D256_RESID = int(os.environ.get("LSD_D256_RESID", "0"))  # residual projections too
     TILED_MIN_N = int(os.environ.get("LSD_TILED_MIN_N", "4000"))
+    # 128x64 decode ring on 8 waves (gemm.hip gemm_ring8_kernel): 0 = the
+    # 4-wave ring, 1 = 4 computing + 4 loader waves, 2 = 8 computing waves.
+    # 256 rows (tools/bench_d256.py, profiles/r3_ring8_ab.log): GPT-2 XL QKV
+    # 16.7 -> 15.2 us, MLP-up 17.5 -> 15.8, residual projections 3-6 %
+    # faster; bench 48.9k -> 49.7k tok/s (p50 8.54 -> 8.38 ms).  A 4-slot
+    # ring is faster alone (QKV 14.4 us) but slower beside the other lane
+    # (p50 8.72 ms: 96 KiB of LDS per workgroup), so 3 slots.
+    RING8 = int(os.environ.get("LSD_RING8", "2"))
+    RING8_SLOTS = int(os.environ.get("LSD_RING8_SLOTS", "3"))
 
     def __init__(self):
         self.C = _load()
@@ -207,6 +216,8 @@ class HipBackend(Backend):
         self.C.gemm_set_ring_fill(self.RING_FILL)
         self.C.gemm_set_ring_m96(self.RING_M96)
         self.C.gemm_set_d256_slots(self.D256_SLOTS)
+        self.C.gemm_set_ring8(self.RING8)
+        self.C.gemm_set_ring8_slots(self.RING8_SLOTS)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))

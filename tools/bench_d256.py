@@ -84,13 +84,15 @@ def main():
             resid = kind == "resid"
             act = 0 if resid else kind
 
-            def make(bn, S):
+            def make(bn, S, r8=0):
                 it = [0]
                 x = x0.clone()
 
                 kind = 3 if bn == 128 else 2
 
                 def run():
+                    C.gemm_set_ring8(r8 & 15)  # read at launch (capture) time
+                    C.gemm_set_ring8_slots(r8 >> 4 or 3)
                     w = ws[it[0] % nw]
                     it[0] += 1
                     if resid:
@@ -109,23 +111,29 @@ def main():
                     return C.linear(a, w, bias, act, kind, S, cnt)
                 return run
 
-            cases = [("ring", 0, 1)]
+            cases = [("ring", 0, 1, 0)]
             for v in variants:
+                if v.startswith("r8:"):  # 8-wave ring layouts (gemm_ring8_kernel): r8:VAR[:SLOTS]
+                    f = [int(x) for x in v[3:].split(":")]
+                    code = f[0] + 16 * (f[1] if len(f) > 1 else 3)
+                    cases.append((f"ring8v{f[0]}s{f[1] if len(f) > 1 else 3}", 0, 1, code))
+                    continue
                 bn, S = map(int, v.split(":"))
                 if S > K // 64 // 2 or (bn == 128 and N % 128):
                     continue
-                cases.append((f"d{bn}s{S}", bn, S))
+                cases.append((f"d{bn}s{S}", bn, S, 0))
             # correctness vs the production path (same weight, fresh residual)
             outs = []
-            for _, bn, S in cases:
-                f = make(bn, S)
+            for _, bn, S, r8 in cases:
+                f = make(bn, S, r8)
                 y = f()
                 torch.cuda.synchronize()
                 outs.append((y - x0) if resid else y.float())
             base = outs[0]
             diffs = [float((o - base).abs().max()) for o in outs]
-            times = graph_time([make(bn, S) for _, bn, S in cases])
-            for (lab, bn, S), t, d in zip(cases, times, diffs):
+            times = graph_time([make(bn, S, r8) for _, bn, S, r8 in cases])
+            C.gemm_set_ring8(0)
+            for (lab, bn, S, _), t, d in zip(cases, times, diffs):
                 row = {"M": M, "shape": name, "N": N, "K": K, "case": lab,
                        "us_med": round(statistics.median(t), 2), "us_min": round(min(t), 2),
                        "wTB/s": round(nbytes / (statistics.median(t) * 1e-6) / 1e12, 3),
