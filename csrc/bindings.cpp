@@ -28,8 +28,9 @@ void lsd_gemm_set_ring_fill(int v);
 void lsd_gemm_set_ring_m96(int v);
 void lsd_gemm_set_d256_slots(int v);
 void lsd_gemm_set_ring8(int v);
-void lsd_gemm_set_ring8_slots(int v);
+void lsd_gemm_set_ring8_flags(int v);
 int lsd_gemm_d256_bn(int kind, int M, int N, int K);
+int lsd_gemm_ring8_tiles(int M, int N, int K, int S);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
 void lsd_attn_set_large_waves(int hd, int v);
@@ -142,18 +143,22 @@ void run_gemm(GemmParams& p, int epi, int64_t tiled, int64_t splits,
   float* ws = nullptr;
   torch::Tensor wsbuf;
   if (tiled && splits > 1 && epi != EPI_SLAB) {
-    // tiled split-K with an in-kernel combine: only the 256-row decode kernel
-    // (gemm_d256) has one -- ticket counters + fp32 partial tiles per split
+    // tiled split-K with an in-kernel combine: the 256-row decode kernel
+    // (gemm_d256, kind 2 / 3) or the 8-wave 128x64 ring (kind 1) -- ticket
+    // counters + fp32 partial tiles per split
     const int bn = lsd_gemm_d256_bn((int)tiled, p.M, p.N, p.K);
-    TORCH_CHECK(bn > 0, what, ": tiled split-K with an in-kernel combine needs the 256-row kernel (kind 2 / 3)");
-    const long tiles = (p.N + bn - 1) / bn;
+    const int r8 = tiled == 1 ? lsd_gemm_ring8_tiles(p.M, p.N, p.K, (int)splits) : 0;
+    TORCH_CHECK(bn > 0 || r8 > 0, what, ": tiled split-K with an in-kernel combine needs the 256-row "
+                "kernel (kind 2 / 3) or the 8-wave decode ring");
+    const long tiles = r8 > 0 ? r8 : (p.N + bn - 1) / bn;
+    const long tile_floats = r8 > 0 ? 128L * 64 : 256L * bn;
     TORCH_CHECK(counters.has_value(), what, ": split-K needs the ticket counter buffer");
     need(*counters, torch::kInt32, "counters");
     TORCH_CHECK(counters->is_contiguous() && counters->numel() >= tiles,
                 what, ": counter buffer too small (", counters->numel(), " < ", tiles, ")");
     cnt = counters->data_ptr<int>();
-    TORCH_CHECK(splits * 256L * bn * 4 < (1L << 31), what, ": split workspace too large");
-    wsbuf = torch::empty({tiles * splits * 256 * bn}, like.options().dtype(torch::kFloat32));
+    TORCH_CHECK(splits * tile_floats * 4 < (1L << 31), what, ": split workspace too large");
+    wsbuf = torch::empty({tiles * splits * tile_floats}, like.options().dtype(torch::kFloat32));
     ws = wsbuf.data_ptr<float>();
   }
   if (!tiled && epi != EPI_SLAB) {
@@ -629,7 +634,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // gemm_d256 (launch kind 2 / 3: all <= 256 rows in one tile, 64 / 128 columns): ring depth
   m.def("gemm_set_d256_slots", [](int64_t v) { lsd_gemm_set_d256_slots((int)v); });
   m.def("gemm_set_ring8", [](int64_t v) { lsd_gemm_set_ring8((int)v); });
-  m.def("gemm_set_ring8_slots", [](int64_t v) { lsd_gemm_set_ring8_slots((int)v); });
+  m.def("gemm_ring8_tiles", [](int64_t M, int64_t N, int64_t K, int64_t S) {
+    return (int64_t)lsd_gemm_ring8_tiles((int)M, (int)N, (int)K, (int)S);
+  });
+  m.def("gemm_set_ring8_flags", [](int64_t v) { lsd_gemm_set_ring8_flags((int)v); });
   m.def("gemm_d256_bn", [](int64_t kind, int64_t M, int64_t N, int64_t K) {
     return lsd_gemm_d256_bn((int)kind, (int)M, (int)N, (int)K);
   });

@@ -736,7 +736,7 @@ __global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_
 
 // Stage a [ROWS][64 k] tile (the lds_frag image) with NWAVES waves sharing
 // the ROWS / 8 wave-instructions; `wi` = this wave's index among them.
-template <int ROWS, int NWAVES>
+template <int ROWS, int NWAVES, int AUX = 0>
 __device__ __forceinline__ void stage_rows(char* lds_tile, const bf16* src, long ld, int row0, int row_max,
                                            int k0, int wi) {
   const int lane = lane_id();
@@ -748,7 +748,7 @@ __device__ __forceinline__ void stage_rows(char* lds_tile, const bf16* src, long
     const int row = inst * 8 + (lane >> 3);
     const int lch = (lane & 7) ^ ((row >> 1) & 7);
     const bf16* gp = src + (long)min(row0 + row, row_max) * ld + k0 + lch * 8;
-    __builtin_amdgcn_global_load_lds((gbl_cvoid*)gp, (lds_void*)(lds_tile + inst * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)gp, (lds_void*)(lds_tile + inst * 1024), 16, 0, AUX);
   }
 }
 
@@ -762,8 +762,24 @@ __device__ __forceinline__ void stage_rows(char* lds_tile, const bf16* src, long
 //   VAR 2: all 8 waves compute 32 x 32 and each issues 3 glds per step.
 // One raw s_barrier per k-step publishes step kt's slot (every loader waited
 // its own DMAs with a counted vmcnt) and proves step kt-1's slot free.
-template <int EPI, int VAR, int SLOTS>
-__global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles_m, int tiles_n) {
+// A/B knobs: NTW = weights staged non-temporal (aux nt: once-read bytes,
+// microarch 'nt-weights'); rot = each tile starts its K loop at a different
+// k-step (tile-dependent rotation, fixed per tile, so results stay
+// deterministic) so that the workgroups of an XCD do not all read the same
+// A k-slice at the same time.
+//
+// K splits (p.splits > 1): EPI_SLAB writes its partial slab (residual
+// projections; the next norm folds the slabs).  Any other epilogue (QKV /
+// MLP-up at 129-256 rows, VAR 2 only): every split publishes its fp32
+// partial tile write-through (sc1 stores) in a lane-major layout (each
+// thread's 16-byte accumulators contiguous across the workgroup: whole-line
+// stores and loads), takes an agent-scope ticket, and the last-arriving split
+// reloads the other partials (sc1 loads) and sums all S in split order
+// (deterministic) before the fused epilogue (guide §5 "In-launch split-K
+// reduction", sc1 form: no release / acquire fences).
+template <int EPI, int VAR, int SLOTS, int NTW = 0>
+__global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles_m, int tiles_n, int rot,
+                                                         int* __restrict__ cnt, float* __restrict__ ws) {
   constexpr int D = SLOTS - 1, TN = 64, TM = TBM;
   constexpr int CW = VAR == 1 ? 4 : 8;           // computing waves
   constexpr int LWN = VAR == 1 ? 4 : 8;          // loading waves
@@ -800,10 +816,13 @@ __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles
 #pragma unroll
     for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const int nk = ke - kb, r0 = rot && nk > 0 ? (t * 7) % nk : 0;
   auto issue = [&](int kt, int slot) {
     char* b = smem + slot * SLOT_BYTES;
-    stage_rows<TM, LWN>(b, p.A, p.lda, m0, p.M - 1, kt * TBK, lw);
-    stage_rows<TN, LWN>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, kt * TBK, lw);
+    int k = kt - kb + r0;
+    k = kb + (k >= nk ? k - nk : k);
+    stage_rows<TM, LWN>(b, p.A, p.lda, m0, p.M - 1, k * TBK, lw);
+    stage_rows<TN, LWN, NTW ? 2 : 0>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, k * TBK, lw);
   };
   if (loader) {
 #pragma unroll
@@ -840,6 +859,66 @@ __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles
     slot = slot == SLOTS - 1 ? 0 : slot + 1;
   }
   __syncthreads();  // fragment reads retired (and no DMA pending) before the C tile overwrites the slots
+  if constexpr (VAR == 2 && EPI != EPI_SLAB) {
+    const int S = p.splits;
+    if (S > 1) {
+      constexpr int PER = MI * JT * 512;  // f32x4 per split tile
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          ws + (long)t * S * PER * 4, (short)0, S * PER * 16, 0x00020000);
+      const int toff = threadIdx.x * 16;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                                 split * PER * 16 + (i * JT + j) * 8192 + toff, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* s_flag = reinterpret_cast<int*>(smem);
+      if (threadIdx.x == 0) {
+        const int tk = __hip_atomic_fetch_add(cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = (tk == S - 1);
+        if (tk == S - 1) __hip_atomic_store(cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (*s_flag == 0) return;
+      __syncthreads();  // every wave has read the flag before the C tile overwrites it
+      // every partial of a group in flight before the adds (its own one too:
+      // no per-load register-or-load select); clamped split index x 0/1 mask,
+      // no per-load branch (guide §5 trap (c))
+      constexpr int RG = 4;
+      f32x4 sum[MI][JT];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s0 = 0; s0 < S; s0 += RG) {
+        f32x4 v[RG][MI][JT];
+#pragma unroll
+        for (int u = 0; u < RG; ++u) {
+          const int s2 = min(s0 + u, S - 1);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < JT; ++j)
+              v[u][i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                  rs, s2 * PER * 16 + (i * JT + j) * 8192 + toff, 0, 16));
+        }
+#pragma unroll
+        for (int u = 0; u < RG; ++u) {
+          const float msk = (s0 + u < S) ? 1.f : 0.f;
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < JT; ++j) sum[i][j] += v[u][i][j] * msk;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j) acc[i][j] = sum[i][j];
+    }
+  }
   float* ct = reinterpret_cast<float*>(smem);
   if (compute) {
 #pragma unroll
@@ -1543,7 +1622,8 @@ static int g_ring_fill = 128; // auto: 32-wide tiles below this many 64-wide wor
 static int g_ring_m96 = 0;    // lsd_gemm_set_ring_m96(): largest 96-row-tile ring grid (0 = off)
 // lsd_gemm_set_ring8(): 128x64 decode ring on 8 waves (gemm_ring8_kernel): 0 off, 1 loader waves, 2 all compute
 static int g_ring8 = 0;
-static int g_ring8_slots = 3;  // lsd_gemm_set_ring8_slots(): ring depth of layout 2 (3..5)
+// lsd_gemm_set_ring8_flags(): A/B bits, 1 = rotate each tile's K start, 2 = weights staged nt
+static int g_ring8_flags = 0;
 static int g_d256_slots = 3;  // lsd_gemm_set_d256_slots(): gemm_d256 ring depth 2..4 (BN 128: at most 3)
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
@@ -1636,7 +1716,7 @@ static hipError_t launch_d256(const GemmParams& p, int kind, int* cnt, float* ws
 }
 
 template <int EPI>
-static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
+static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
   // 256x256 pipelined kernel once the problem fills the chip with 1-block/CU
   // tiles; the 128x128 kernel (2 blocks/CU) for smaller M / N.
   const int bm = (p.M + GBM - 1) / GBM, bn = (p.N + GBN - 1) / GBN;
@@ -1679,14 +1759,15 @@ static hipError_t launch_tiled(const GemmParams& p, hipStream_t st) {
     }
     if (tm * tn64 * p.splits <= g_tiled3_max_blocks) {
       const dim3 g8(tm * tn64 * p.splits), b8(512);
+      const int rot = (g_ring8_flags & 1) != 0;
+      const bool combine = p.splits > 1 && EPI != EPI_SLAB;
+      if (combine && (g_ring8 != 2 || cnt == nullptr || ws == nullptr)) return hipErrorInvalidValue;
       if (g_ring8 == 1)
-        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 1, 3>), g8, b8, 0, st, p, tm, tn64);
-      else if (g_ring8 == 2 && g_ring8_slots == 4)
-        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 4>), g8, b8, 0, st, p, tm, tn64);
-      else if (g_ring8 == 2 && g_ring8_slots == 5)
-        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 5>), g8, b8, 0, st, p, tm, tn64);
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 1, 3>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
+      else if (g_ring8 == 2 && (g_ring8_flags & 2))
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 1>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else if (g_ring8 == 2)
-        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3>), g8, b8, 0, st, p, tm, tn64);
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else
         hipLaunchKernelGGL((gemm_ring_kernel<EPI, 3, 64>), dim3(tm * tn64 * p.splits), dim3(256), 0, st, p, tm, tn64);
       return hipGetLastError();
@@ -1720,11 +1801,24 @@ extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 ||
 extern "C" void lsd_gemm_set_ring_fill(int v) { g_ring_fill = v; }
 extern "C" void lsd_gemm_set_ring_m96(int v) { g_ring_m96 = v; }
 extern "C" void lsd_gemm_set_ring8(int v) { g_ring8 = (v == 1 || v == 2) ? v : 0; }
-extern "C" void lsd_gemm_set_ring8_slots(int v) { g_ring8_slots = v < 3 ? 3 : (v > 5 ? 5 : v); }
+extern "C" void lsd_gemm_set_ring8_flags(int v) { g_ring8_flags = v & 3; }
 extern "C" void lsd_gemm_set_d256_slots(int v) { g_d256_slots = v < 2 ? 2 : (v > 4 ? 4 : v); }
 // columns per gemm_d256 tile of a launch of this kind (0: not a d256 launch):
 // the split workspace and ticket counters are sized from it (bindings.cpp)
 extern "C" int lsd_gemm_d256_bn(int kind, int M, int N, int K) { return d256_bn(kind, M, N, K); }
+// 128x64 tiles of a tiled (kind 1) launch when it runs on gemm_ring8_kernel
+// (mirrors launch_tiled), else 0: the split workspace / counters are sized from it
+extern "C" int lsd_gemm_ring8_tiles(int M, int N, int K, int S) {
+  if (g_ring8 != 2) return 0;
+  const int bm = (M + GBM - 1) / GBM, bn = (N + GBN - 1) / GBN;
+  if (M >= GBM && K % 64 == 0 && bm * bn * S >= g_big_min_blocks) return 0;
+  if (!(g_ring_tn == 64 || g_ring_tn == 32 || g_ring_tn == 0)) return 0;
+  const int tm = (M + TBM - 1) / TBM, tn64 = (N + 63) / 64;
+  const bool narrow = g_ring_tn == 32 || (g_ring_tn == 0 && tm * tn64 * S < g_ring_fill);
+  if (narrow && (N % 32) == 0 && tm * ((N + 31) / 32) * S <= 2 * g_tiled3_max_blocks) return 0;
+  if (S == 1 && M > TBM && g_ring_m96 > 0 && ((M + 95) / 96) * tn64 <= g_ring_m96) return 0;
+  return tm * tn64 * S <= g_tiled3_max_blocks ? tm * tn64 : 0;
+}
 extern "C" int lsd_gemm_sk_rblocks(int M, int N, int S) { return sk_rblocks(M, N, S); }
 extern "C" int lsd_gemm_sk_rows(int M, int N, int S) {  // rows per row block
   return sk_mt(M, sk_rblocks(M, N, S)) * 16;
@@ -1739,7 +1833,7 @@ extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int kind, int* cnt,
 #define LSD_DISPATCH(E)                                                                   \
   case E:                                                                                 \
     return kind >= 2 ? launch_d256<E>(*p, kind, cnt, ws, st)                              \
-                     : (kind ? launch_tiled<E>(*p, st) : launch_sk<E>(*p, cnt, ws, st));
+                     : (kind ? launch_tiled<E>(*p, cnt, ws, st) : launch_sk<E>(*p, cnt, ws, st));
   switch (epi) {
     LSD_DISPATCH(EPI_BF16)
     LSD_DISPATCH(EPI_GELU)

@@ -204,7 +204,11 @@ class HipBackend(Backend):
     # ring is faster alone (QKV 14.4 us) but slower beside the other lane
     # (p50 8.72 ms: 96 KiB of LDS per workgroup), so 3 slots.
     RING8 = int(os.environ.get("LSD_RING8", "2"))
-    RING8_SLOTS = int(os.environ.get("LSD_RING8_SLOTS", "3"))
+    RING8_FLAGS = int(os.environ.get("LSD_RING8_FLAGS", "0"))  # A/B bits (gemm.hip)
+    # K splits of the non-residual decode GEMMs on the 8-wave ring (QKV, MLP-up,
+    # 129-256 rows) with the in-kernel last-arriver combine: aim at this many
+    # workgroups (0 = off: one workgroup per 128x64 tile)
+    RING8_SK_TARGET = int(os.environ.get("LSD_RING8_SK_TARGET", "0"))
 
     def __init__(self):
         self.C = _load()
@@ -217,7 +221,7 @@ class HipBackend(Backend):
         self.C.gemm_set_ring_m96(self.RING_M96)
         self.C.gemm_set_d256_slots(self.D256_SLOTS)
         self.C.gemm_set_ring8(self.RING8)
-        self.C.gemm_set_ring8_slots(self.RING8_SLOTS)
+        self.C.gemm_set_ring8_flags(self.RING8_FLAGS)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))
@@ -348,8 +352,19 @@ class HipBackend(Backend):
         if bn:
             return self._d256_kind(bn), self._d256_splits(N, K, bn, self.D256_TARGET)
         if self._tiled(M, N):
-            return True, 1
+            return True, self._ring8_splits(M, N, K)
         return False, self._sk_splits(M, N, K, nw)
+
+    def _ring8_splits(self, M: int, N: int, K: int) -> int:
+        """K splits of a non-residual tiled decode GEMM on the 8-wave ring (1:
+        unsplit; the host routing check is gemm.hip lsd_gemm_ring8_tiles)."""
+        if not (self.RING8 == 2 and self.RING8_SK_TARGET and 128 < M <= self.SK_MAX_M and K % 64 == 0):
+            return 1
+        tiles = math.ceil(M / 128) * math.ceil(N / 64)
+        S = max(1, min(round(self.RING8_SK_TARGET / tiles), K // 64 // 4, 4))
+        if S > 1 and not self.C.gemm_ring8_tiles(M, N, K, S):
+            return 1
+        return S
 
     # ------------------------------------------------------------------
     def embed(self, ids, pos, wte, wpe):

@@ -112,7 +112,7 @@ class Engine:
         self._stop_loop = threading.Event()
         self._wake = threading.Event()  # a request was submitted (serving loop)
         # LSD_HOST_PROFILE=1: host seconds in (plan, issue, readout wait), steps
-        self._hostprof = [0.0, 0.0, 0.0, 0, 0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
+        self._hostprof = [0.0, 0.0, 0.0, 0, 0, 0.0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
         self.kv_slots = 0
 
         if mode == "local":
@@ -364,8 +364,10 @@ class Engine:
                 nxt = sch.build_step()
                 self._send_plans(nxt)
                 t1 = time.monotonic()
+                c1 = time.thread_time() if hp is not None else 0.0
                 w0.run_step(cur[0], nxt[0] if nxt is not None else None)
                 t2 = time.monotonic()
+                c2 = time.thread_time() if hp is not None else 0.0
                 sch.poll(block_until_step=cur[0].step - lag)
                 if hp is not None and not any(gp.chunks for gp in cur[0].groups):
                     t3 = time.monotonic()  # decode steps only (prefill issue is eager)
@@ -374,6 +376,7 @@ class Engine:
                     hp[2] += t3 - t2
                     hp[3] += 1
                     hp[4] += sum(1 for gp in cur[0].groups if gp.has_work)
+                    hp[5] += c2 - c1  # CPU time of the issuing thread (no waits)
                 cur = nxt
             if ran:
                 w0.end_session()
@@ -523,7 +526,10 @@ class Engine:
                 return
             step, key, host, ev = item
             if ev is not None:
-                ev.synchronize()
+                from ..parallel.pipeline import GPU_GATE
+
+                with GPU_GATE.shared():  # not beside a stage thread's capture
+                    ev.synchronize()
             if delay:
                 time.sleep(delay)
             self.tok_ch.send(0, (step, key, host.tolist()))

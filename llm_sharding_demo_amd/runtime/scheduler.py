@@ -533,11 +533,25 @@ class Scheduler:
         key = (plan.replica, plan.step, gp.g)
         n = gp.ret
         if ret.is_cuda:
+            from ..parallel.pipeline import GPU_GATE
+
             host = torch.empty(n, dtype=torch.int32, pin_memory=True)
             host.copy_(ret[:n], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
-            self.readouts.append((plan.step, ev.query, ev.synchronize, host, key))
+
+            # the coordinator thread polls these beside the stage threads: never
+            # in the middle of a sibling's hipGraph capture (HIP refuses event
+            # queries then -- hipErrorCapturedEvent -- and invalidates the
+            # capture), so each query / wait holds the capture gate shared
+            def ready(ev=ev):
+                with GPU_GATE.shared():
+                    return ev.query()
+
+            def sync(ev=ev):
+                with GPU_GATE.shared():
+                    ev.synchronize()
+            self.readouts.append((plan.step, ready, sync, host, key))
         else:
             host = ret[:n].clone()
             self.readouts.append((plan.step, lambda: True, lambda: None, host, key))

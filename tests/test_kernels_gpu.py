@@ -235,6 +235,53 @@ def test_ring_gemm_96_row_tiles(C, CNT, M, K):
         C.gemm_set_ring_tn(128)
 
 
+@pytest.fixture(params=[(1, 0), (2, 0), (2, 1), (2, 2)])
+def RING8(C, request):
+    """128x64 decode ring on 8 waves (gemm_ring8_kernel): (layout, A/B flags)
+    -- 1 = 4 computing + 4 loader waves, 2 = 8 computing waves; flag 1 =
+    rotated K start per tile, 2 = nt weight staging."""
+    var, flags = request.param
+    C.gemm_set_tiled3_max(1 << 30)
+    C.gemm_set_ring_tn(64)
+    C.gemm_set_ring8(var)
+    C.gemm_set_ring8_flags(flags)
+    yield C, var
+    C.gemm_set_ring8(0)
+    C.gemm_set_ring8_flags(0)
+    C.gemm_set_tiled3_max(0)
+    C.gemm_set_ring_tn(128)
+
+
+@pytest.mark.parametrize("M", [100, 200, 256])
+@pytest.mark.parametrize("K,splits", [(64, 1), (192, 1), (640, 1), (640, 2), (1600, 1), (1600, 3), (1600, 4)])
+def test_ring8_gemm_epilogues(RING8, CNT, M, K, splits):
+    """8-wave decode ring: every epilogue, M / N tails, 1 to 25 k-steps,
+    in-kernel split-K combine (8 computing waves) bit-stable across launches
+    that reuse the re-armed ticket counters, residual slabs folded by the norm."""
+    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
+
+    C, var = RING8
+    if splits > 1 and var != 2:
+        pytest.skip("the split-K combine is built for the 8-computing-wave layout")
+    N = 352  # 5.5 tiles of 64 columns: a partial last tile
+    a, w, bias = bf(M, K, seed=90), bf(N, K, scale=0.05, seed=91), bf(N, scale=0.1, seed=92)
+    y_ref = ref.linear(a, w, bias)
+    y1 = C.linear(a, w, bias, 0, True, splits, CNT)
+    close(y1, y_ref, 3e-2)
+    assert torch.equal(C.linear(a, w, bias, 0, True, splits, CNT), y1)
+    close(C.linear(a, w, bias, 1, True, splits, CNT), ref.gelu_new(y_ref), 3e-2)
+    w2 = w[:256].contiguous()
+    y = C.linear(a, interleave_gate_up(w2, 128).contiguous(), None, 2, True, splits, CNT)
+    close(y, ref.silu_mul(*ref.linear(a, w2).split(128, 1)), 3e-2)
+    close(C.linear_f32(a, w, True, splits, CNT), ref.linear(a, w), 2e-3, 1e-3)
+    x = torch.randn(M, N, device=DEV)
+    x_ref = x + y_ref
+    slab = C.linear_residual(a, w, bias, x, splits, True, CNT, False)
+    if splits > 1:
+        C.norm(x, slab, bias, None, None, 0.0, True, None, False)
+    close(x, x_ref, 2e-3, 1e-3)
+
+
 @pytest.fixture(params=[(2, 3), (3, 3), (2, 2), (2, 4), (3, 2)])
 def D256(C, request):
     """(launch kind, ring slots) of the 8-wave all-rows kernel gemm_d256:

@@ -92,7 +92,7 @@ def main():
 
                 def run():
                     C.gemm_set_ring8(r8 & 15)  # read at launch (capture) time
-                    C.gemm_set_ring8_slots(r8 >> 4 or 3)
+                    C.gemm_set_ring8_flags(r8 >> 4)
                     w = ws[it[0] % nw]
                     it[0] += 1
                     if resid:
@@ -105,18 +105,24 @@ def main():
                         if slab is not None:
                             C.norm(x, slab, bias, None, None, 0.0, True, None, False)
                         return x
+                    if bn < 0:  # ring8 split-K
+                        return C.linear(a, w, bias, act, 1, -bn, cnt)
                     if bn == 0:
                         tiled, s2 = be._gemm_kw(M, N, K, 2 if act == 2 else 1)
                         return C.linear(a, w, bias, act, tiled, s2, cnt)
                     return C.linear(a, w, bias, act, kind, S, cnt)
                 return run
 
-            cases = [("ring", 0, 1, 0)]
+            cases = [("ring", 0, 1, int(os.environ.get("D256_BASE_R8", "0")))]
             for v in variants:
-                if v.startswith("r8:"):  # 8-wave ring layouts (gemm_ring8_kernel): r8:VAR[:SLOTS]
+                if v.startswith("r8s:"):  # 8-wave ring, S K splits + in-kernel combine
+                    if not resid:
+                        cases.append((f"ring8s{v[4:]}", -int(v[4:]), 1, 2))
+                    continue
+                if v.startswith("r8:"):  # 8-wave ring layouts (gemm_ring8_kernel): r8:VAR[:FLAGS]
                     f = [int(x) for x in v[3:].split(":")]
-                    code = f[0] + 16 * (f[1] if len(f) > 1 else 3)
-                    cases.append((f"ring8v{f[0]}s{f[1] if len(f) > 1 else 3}", 0, 1, code))
+                    code = f[0] + 16 * (f[1] if len(f) > 1 else 0)
+                    cases.append((f"ring8v{f[0]}f{f[1] if len(f) > 1 else 0}", 0, 1, code))
                     continue
                 bn, S = map(int, v.split(":"))
                 if S > K // 64 // 2 or (bn == 128 and N % 128):
