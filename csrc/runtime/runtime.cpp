@@ -18,6 +18,7 @@
 //                        admission into slots, per-step group plans (leaves,
 //                        joins, prefill chunks, decode rows / buckets), token
 //                        readout events and slot release.
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -107,6 +108,13 @@ PYBIND11_MODULE(_runtime, m) {
            }, py::arg("step"))
       .def("assign", &SchedCore::assign, py::arg("rep"), py::arg("step"), py::arg("g"),
            py::arg("tokens"), py::arg("eos"))
+      .def("assign_collect",
+           [](SchedCore& c, int rep, int64_t step, int g,
+              py::array_t<int32_t, py::array::c_style | py::array::forcecast> tokens, int eos) {
+             auto r = tokens.unchecked<1>();
+             return c.assign_collect(rep, step, g, r.shape(0) ? r.data(0) : nullptr, (int)r.shape(0), eos);
+           },
+           py::arg("rep"), py::arg("step"), py::arg("g"), py::arg("tokens"), py::arg("eos"))
       .def("reset", &SchedCore::reset)
       .def_property_readonly("joins", &SchedCore::joins)
       .def_property_readonly("leaves", &SchedCore::leaves)

@@ -140,6 +140,35 @@ class SchedCore {
     return ev;
   }
 
+  // assign() for the serving hot path: each sequence's tokens are kept here,
+  // and only FIRST / FINISH / RELEASE events come back (a plain token of a
+  // running sequence costs the caller nothing), plus the whole token list of
+  // every sequence that finished in this readout.  tokens points at n int32
+  // ids (the pinned host copy of the token-return vector).
+  using Finished = std::vector<std::pair<int64_t, std::vector<int>>>;
+  std::pair<std::vector<Event>, Finished> assign_collect(int rep, int64_t step, int g,
+                                                         const int32_t* tokens, int n, int eos) {
+    auto it = expect_.find(key(rep, step, g));
+    if (it == expect_.end()) throw std::runtime_error("no item awaiting this readout");
+    const Produced prod = std::move(it->second);
+    expect_.erase(it);
+    auto tok_at = [&](size_t i) {
+      if ((int)i >= n) throw std::out_of_range("token-return vector shorter than the item's rows");
+      return (int)tokens[i];
+    };
+    std::vector<Event> ev;
+    Finished done;
+    for (size_t i = 0; i < prod.rows.size(); ++i) give_collect(prod.rows[i], tok_at(i), eos, &ev, &done);
+    for (size_t j = 0; j < prod.finals.size(); ++j)
+      give_collect(prod.finals[j], tok_at(prod.b + j), eos, &ev, &done);
+    for (int64_t sid : prod.release) {
+      auto f = seqs_.find(sid);
+      if (f != seqs_.end() && !f->second.finished) done.emplace_back(sid, f->second.toks);
+      release(sid, &ev);
+    }
+    return {std::move(ev), std::move(done)};
+  }
+
   // Drop every sequence and give their slots back (failure path).
   void reset() {
     for (auto& kv : seqs_)
@@ -165,6 +194,7 @@ class SchedCore {
     int prompt_len = 0, prefilled = 0, issued = 0, pos = 0, sstep = 1;
     int want = 0, ntok = 0;
     bool stop_at_eos = false, stop = false, finished = false;
+    std::vector<int> toks;  // assign_collect only
   };
   struct Produced {
     int b = 0;
@@ -318,6 +348,23 @@ class SchedCore {
       flags |= EV_FINISH;
     }
     ev->emplace_back(sid, tok, flags);
+  }
+
+  void give_collect(int64_t sid, int tok, int eos, std::vector<Event>* ev, Finished* done) {
+    auto it = seqs_.find(sid);
+    if (it == seqs_.end()) return;
+    Seq& s = it->second;
+    if (s.finished || s.ntok >= s.want) return;
+    int flags = s.ntok == 0 ? EV_FIRST : 0;
+    s.ntok += 1;
+    s.toks.push_back(tok);
+    if (s.stop_at_eos && tok == eos) s.stop = true;
+    if (s.ntok >= s.want || s.stop) {
+      s.finished = true;
+      flags |= EV_FINISH;
+      done->emplace_back(sid, s.toks);
+    }
+    if (flags) ev->emplace_back(sid, tok, flags);
   }
 
   void release(int64_t sid, std::vector<Event>* ev) {

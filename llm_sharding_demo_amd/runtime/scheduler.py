@@ -198,6 +198,7 @@ class _Seq:
     sstep: int = 1              # sampler counter of the next decode draw
     ntok: int = 0               # tokens read back
     stop: bool = False          # EOS read back (stop_at_eos): leave at the next step
+    toks: List[int] = field(default_factory=list)  # assign_collect only
     finished: bool = False
 
 
@@ -375,6 +376,43 @@ class PySchedCore:
                 self.pools[s.rep].free([s.slot])
             ev.append((sid, -1, EV_RELEASE | (0 if s.finished else EV_FINISH)))
         return ev
+
+    def assign_collect(self, rep: int, step: int, g: int, tokens, eos: int):
+        """Twin of SchedCore::assign_collect: only FIRST / FINISH / RELEASE
+        events, plus (sid, tokens) of every sequence that finished."""
+        prod = self.expect.pop((rep, step, g))
+        tokens = [int(t) for t in tokens]
+        ev, done = [], []
+        for i, sid in enumerate(prod.rows):
+            self._give_collect(sid, tokens[i], eos, ev, done)
+        for j, sid in enumerate(prod.finals):
+            self._give_collect(sid, tokens[prod.b + j], eos, ev, done)
+        for sid in prod.release:
+            s = self.seqs.pop(sid, None)
+            if s is None:
+                continue
+            if not s.finished:
+                done.append((sid, list(s.toks)))
+            if s.slot >= 0:
+                self.pools[s.rep].free([s.slot])
+            ev.append((sid, -1, EV_RELEASE | (0 if s.finished else EV_FINISH)))
+        return ev, done
+
+    def _give_collect(self, sid: int, tok: int, eos: int, ev: list, done: list) -> None:
+        s = self.seqs.get(sid)
+        if s is None or s.finished or s.ntok >= s.want:
+            return
+        flags = EV_FIRST if s.ntok == 0 else 0
+        s.ntok += 1
+        s.toks.append(tok)
+        if s.stop_at_eos and tok == eos:
+            s.stop = True
+        if s.ntok >= s.want or s.stop:
+            s.finished = True
+            flags |= EV_FINISH
+            done.append((sid, list(s.toks)))
+        if flags:
+            ev.append((sid, tok, flags))
 
     def _give(self, sid: int, tok: int, eos: int, ev: list) -> None:
         s = self.seqs.get(sid)
@@ -574,34 +612,33 @@ class Scheduler:
             self._assign(host, key)
 
     def _assign(self, host: torch.Tensor, key) -> None:
-        """Apply one group readout: one event per row (plain tokens are the
-        common case and take the short path -- at 16 groups x 256 rows per
-        step this loop is the largest host cost of stage 0)."""
+        """Apply one group readout.  The core keeps every sequence's tokens
+        (assign_collect): a plain token of a running sequence costs nothing
+        here, only first tokens (TTFT), finishes and slot releases come back --
+        a per-row Python loop at 16 groups x 256 rows per step used to be
+        stage 0's largest host cost (profiles/r3_rehearsal_all_configs.log)."""
         rep, step, g = key
-        events = self.core.assign(rep, step, g, host.tolist(), self.eng.mcfg.eos_token_id)
+        events, done = self.core.assign_collect(rep, step, g, host.numpy(), self.eng.mcfg.eos_token_id)
+        if not events:
+            return
         now = time.monotonic()
+        done = dict(done)
         get = self.meta.get
         for sid, tok, flags in events:
-            if not flags:
-                m = get(sid)
-                if m is not None and not m.done:
-                    m.tokens.append(tok)
-                continue
             if flags & EV_RELEASE:
                 m = self.meta.pop(sid, None)
                 if m is not None and flags & EV_FINISH and not m.done:
                     m.done = True
-                    m.req.finish(list(m.tokens))
+                    m.req.finish(done.get(sid, []))
                 continue
             m = get(sid)
             if m is None or m.done:
                 continue
             if flags & EV_FIRST:
                 m.req.t_first = now
-            m.tokens.append(tok)
             if flags & EV_FINISH:
                 m.done = True
-                m.req.finish(list(m.tokens))
+                m.req.finish(done[sid])
 
     # -- failure -----------------------------------------------------------------
     def fail_all(self, err: BaseException) -> None:

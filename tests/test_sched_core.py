@@ -23,8 +23,9 @@ def _rt():
     return rt
 
 
+@pytest.mark.parametrize("collect", [False, True])
 @pytest.mark.parametrize("seed", range(12))
-def test_native_core_matches_python_twin(seed):
+def test_native_core_matches_python_twin(seed, collect):
     rt = _rt()
     rnd = random.Random(seed)
     R, M = rnd.choice([1, 2]), rnd.choice([1, 2, 3])
@@ -39,6 +40,7 @@ def test_native_core_matches_python_twin(seed):
     py = PySchedCore(R, M, cap, budget, chunk, max_seq, ppool)
     sid = 0
     pending = []  # (step, rep, g, n_tokens)
+    got, fed = {}, {}  # finished token lists (collect) / tokens from plain events
     for step in range(400):
         if step < 150 and rnd.random() < 0.3:
             for _ in range(rnd.randint(1, 4)):
@@ -63,15 +65,38 @@ def test_native_core_matches_python_twin(seed):
         while pending and pending[0][0] <= step - lag:
             st, rep, g, n = pending.pop(0)
             toks = [rnd.choice([eos, 11, 12, 13]) for _ in range(n)]
-            en = [tuple(e) for e in nat.assign(rep, st, g, toks, eos)]
-            ep = py.assign(rep, st, g, toks, eos)
-            assert en == ep
+            if collect:  # the serving fast path: tokens kept in the core
+                import numpy as np
+
+                en, dn = nat.assign_collect(rep, st, g, np.array(toks, dtype=np.int32), eos)
+                ep, dp = py.assign_collect(rep, st, g, toks, eos)
+                assert [tuple(e) for e in en] == ep and [(a, list(b)) for a, b in dn] == dp
+                assert all(e[2] for e in ep)  # plain tokens never come back
+                for sid_, tl in dp:
+                    got.setdefault(sid_, tl)
+            else:
+                en = [tuple(e) for e in nat.assign(rep, st, g, toks, eos)]
+                ep = py.assign(rep, st, g, toks, eos)
+                assert en == ep
+                for e in ep:
+                    if e[1] >= 0:
+                        fed.setdefault(e[0], []).append(e[1])
         assert [p.available for p in npool] == [p.available for p in ppool]
         assert (nat.joins, nat.leaves, nat.max_rows) == (py.joins, py.leaves, py.max_rows)
     while pending:
         st, rep, g, n = pending.pop(0)
-        assert [tuple(e) for e in nat.assign(rep, st, g, [11] * n, eos)] == py.assign(rep, st, g, [11] * n, eos)
+        if collect:
+            import numpy as np
+
+            en, dn = nat.assign_collect(rep, st, g, np.full(n, 11, dtype=np.int32), eos)
+            ep, dp = py.assign_collect(rep, st, g, [11] * n, eos)
+            assert [tuple(e) for e in en] == ep and [(a, list(b)) for a, b in dn] == dp
+        else:
+            assert [tuple(e) for e in nat.assign(rep, st, g, [11] * n, eos)] == py.assign(rep, st, g, [11] * n, eos)
     assert nat.n_expect == py.n_expect == 0
+    # a finished sequence's list holds between 1 and `want` (<= 20) tokens
+    for tl in got.values():
+        assert 1 <= len(tl) <= 20
 
 
 def test_native_core_release_and_reset():

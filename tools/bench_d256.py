@@ -116,7 +116,8 @@ def main():
             cases = [("ring", 0, 1, int(os.environ.get("D256_BASE_R8", "0")))]
             for v in variants:
                 if v.startswith("r8s:"):  # 8-wave ring, S K splits + in-kernel combine
-                    if not resid:
+                    C.gemm_set_ring8(2)
+                    if not resid and C.gemm_ring8_tiles(M, N, K, int(v[4:])):
                         cases.append((f"ring8s{v[4:]}", -int(v[4:]), 1, 2))
                     continue
                 if v.startswith("r8:"):  # 8-wave ring layouts (gemm_ring8_kernel): r8:VAR[:FLAGS]
