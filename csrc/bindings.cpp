@@ -29,6 +29,7 @@ void lsd_gemm_set_ring_m96(int v);
 void lsd_gemm_set_d256_slots(int v);
 void lsd_gemm_set_ring8(int v);
 void lsd_gemm_set_ring8_flags(int v);
+void lsd_gemm_set_ring8_pack(int v);
 int lsd_gemm_d256_bn(int kind, int M, int N, int K);
 int lsd_gemm_ring8_tiles(int M, int N, int K, int S);
 void lsd_attn_set_max_wg(int v);
@@ -599,10 +600,12 @@ void sample_into(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Ten
 }  // namespace
 
 void lsd_register_comm(pybind11::module& m);  // csrc/comm.cpp
+void lsd_register_exec(pybind11::module& m);  // csrc/stage_exec.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "CDNA4 (gfx950) kernels for llm_sharding_demo_amd";
   lsd_register_comm(m);
+  lsd_register_exec(m);
   m.def("linear", &linear);
   m.def("linear_f32", &linear_f32);
   m.def("linear_residual", &linear_residual);
@@ -638,6 +641,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return (int64_t)lsd_gemm_ring8_tiles((int)M, (int)N, (int)K, (int)S);
   });
   m.def("gemm_set_ring8_flags", [](int64_t v) { lsd_gemm_set_ring8_flags((int)v); });
+  m.def("gemm_set_ring8_pack", [](int64_t v) { lsd_gemm_set_ring8_pack((int)v); });
   m.def("gemm_d256_bn", [](int64_t kind, int64_t M, int64_t N, int64_t K) {
     return lsd_gemm_d256_bn((int)kind, (int)M, (int)N, (int)K);
   });

@@ -87,6 +87,11 @@ hipStream_t cur() { return c10::hip::getCurrentHIPStream().stream(); }
 
 }  // namespace
 
+// Raw receive for the native stage executor (csrc/stage_exec.cpp).
+void lsd_rccl_recv_raw(int64_t h, void* ptr, size_t bytes, int peer, hipStream_t st) {
+  check(rccl().recv(ptr, bytes, ncclUint8, peer, as_comm(h), st), "ncclRecv");
+}
+
 void lsd_register_comm(py::module& m) {
   m.def("rccl_version", [] {
     int v = 0;

@@ -752,6 +752,29 @@ __device__ __forceinline__ void stage_rows(char* lds_tile, const bf16* src, long
   }
 }
 
+// Stage the same [ROWS][64 k] image from a k-block-packed operand
+// [K/64][M][64] (activations: every row's 64-k slice of block kb contiguous,
+// rows consecutive -> a tile's k-step is ROWS x 128 B contiguous) or
+// [N/64][K/64][64][64] (weights: one 8 KiB block per 64 rows x 64 k).  Each
+// wave-instruction then reads 1 KiB of consecutive bytes (A/B experiment:
+// the row-strided image reads 8 rows x 128 B at a K x 2 B pitch).
+template <int ROWS, int NWAVES, int WPACK>
+__device__ __forceinline__ void stage_rows_packed(char* lds_tile, const bf16* src, int rows_total, int KB,
+                                                  int row0, int row_max, int kb, int wi) {
+  const int lane = lane_id();
+  constexpr int PER_WAVE = ROWS / 8 / NWAVES;
+#pragma unroll
+  for (int q = 0; q < PER_WAVE; ++q) {
+    const int inst = wi * PER_WAVE + q;
+    const int row = inst * 8 + (lane >> 3);
+    const int lch = (lane & 7) ^ ((row >> 1) & 7);
+    const int r = min(row0 + row, row_max);
+    const bf16* gp = WPACK ? src + (((long)(r >> 6) * KB + kb) << 12) + (r & 63) * 64 + lch * 8
+                           : src + ((long)kb * rows_total + r) * 64 + lch * 8;
+    __builtin_amdgcn_global_load_lds((gbl_cvoid*)gp, (lds_void*)(lds_tile + inst * 1024), 16, 0, 0);
+  }
+}
+
 // 8-wave variant of the 128x64 decode ring (512 threads, same tiles, same
 // 3-slot ring, same grid).  In the 4-wave ring every wave issues its 6 LDS-DMA
 // instructions per k-step (each ~60-185 issue cycles beside MFMAs, microarch
@@ -777,7 +800,7 @@ __device__ __forceinline__ void stage_rows(char* lds_tile, const bf16* src, long
 // reloads the other partials (sc1 loads) and sums all S in split order
 // (deterministic) before the fused epilogue (guide §5 "In-launch split-K
 // reduction", sc1 form: no release / acquire fences).
-template <int EPI, int VAR, int SLOTS, int NTW = 0>
+template <int EPI, int VAR, int SLOTS, int NTW = 0, int PK = 0>
 __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles_m, int tiles_n, int rot,
                                                          int* __restrict__ cnt, float* __restrict__ ws) {
   constexpr int D = SLOTS - 1, TN = 64, TM = TBM;
@@ -821,8 +844,10 @@ __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles
     char* b = smem + slot * SLOT_BYTES;
     int k = kt - kb + r0;
     k = kb + (k >= nk ? k - nk : k);
-    stage_rows<TM, LWN>(b, p.A, p.lda, m0, p.M - 1, k * TBK, lw);
-    stage_rows<TN, LWN, NTW ? 2 : 0>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, k * TBK, lw);
+    if constexpr (PK & 2) stage_rows_packed<TM, LWN, 0>(b, p.A, p.M, p.K / 64, m0, p.M - 1, k, lw);
+    else stage_rows<TM, LWN>(b, p.A, p.lda, m0, p.M - 1, k * TBK, lw);
+    if constexpr (PK & 1) stage_rows_packed<TN, LWN, 1>(b + A_BYTES, p.W, p.N, p.K / 64, n0, p.N - 1, k, lw);
+    else stage_rows<TN, LWN, NTW ? 2 : 0>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, k * TBK, lw);
   };
   if (loader) {
 #pragma unroll
@@ -1624,6 +1649,8 @@ static int g_ring_m96 = 0;    // lsd_gemm_set_ring_m96(): largest 96-row-tile ri
 static int g_ring8 = 0;
 // lsd_gemm_set_ring8_flags(): A/B bits, 1 = rotate each tile's K start, 2 = weights staged nt
 static int g_ring8_flags = 0;
+// lsd_gemm_set_ring8_pack(): operands in k-block-packed layouts (bit 0 W, bit 1 A; A/B only)
+static int g_ring8_pack = 0;
 static int g_d256_slots = 3;  // lsd_gemm_set_d256_slots(): gemm_d256 ring depth 2..4 (BN 128: at most 3)
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
@@ -1764,6 +1791,12 @@ static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStre
       if (combine && (g_ring8 != 2 || cnt == nullptr || ws == nullptr)) return hipErrorInvalidValue;
       if (g_ring8 == 1)
         hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 1, 3>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
+      else if (g_ring8 == 2 && g_ring8_pack == 1)
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 1>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
+      else if (g_ring8 == 2 && g_ring8_pack == 2)
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 2>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
+      else if (g_ring8 == 2 && g_ring8_pack == 3)
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 3>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else if (g_ring8 == 2 && (g_ring8_flags & 2))
         hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 1>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else if (g_ring8 == 2)
@@ -1802,6 +1835,7 @@ extern "C" void lsd_gemm_set_ring_fill(int v) { g_ring_fill = v; }
 extern "C" void lsd_gemm_set_ring_m96(int v) { g_ring_m96 = v; }
 extern "C" void lsd_gemm_set_ring8(int v) { g_ring8 = (v == 1 || v == 2) ? v : 0; }
 extern "C" void lsd_gemm_set_ring8_flags(int v) { g_ring8_flags = v & 3; }
+extern "C" void lsd_gemm_set_ring8_pack(int v) { g_ring8_pack = v & 3; }
 extern "C" void lsd_gemm_set_d256_slots(int v) { g_d256_slots = v < 2 ? 2 : (v > 4 ? 4 : v); }
 // columns per gemm_d256 tile of a launch of this kind (0: not a d256 launch):
 // the split workspace and ticket counters are sized from it (bindings.cpp)

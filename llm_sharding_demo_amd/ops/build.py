@@ -28,8 +28,8 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 KERNELS = ["gemm.hip", "gemv.hip", "norm.hip", "attention.hip", "sample.hip"]
-# host code of the extension: kernel bindings, native RCCL communicator
-HOST_SOURCES = ["bindings.cpp", "comm.cpp"]
+# host code of the extension: kernel bindings, native RCCL communicator, native stage executor
+HOST_SOURCES = ["bindings.cpp", "comm.cpp", "stage_exec.cpp"]
 EXT_NAME = "_C"
 
 

@@ -285,6 +285,8 @@ class StageWorker:
         self.last_stats: Optional[dict] = None
         self.step_events: List[tuple] = []   # stage 0: (step, event) at each step start
         self.readout = None        # stage 0: callable(step, plan, ret_tensor) for token readout
+        # stage 0, native executor: callable(plan, gp, pinned host ids, event, release)
+        self.readout_native = None
         self._tls = threading.local()
         # Decode graphs that contain their own edge receive and send (native
         # RCCL transport, parallel/comm.py RcclTransport): a decode item is
@@ -294,6 +296,16 @@ class StageWorker:
         self.graph_io = bool(transport is not None and getattr(transport, "GRAPH_IO", False)
                              and self.device.type == "cuda"
                              and os.environ.get("LSD_GRAPH_IO", "1") != "0")
+        # Native stage executor (csrc/stage_exec.cpp): a step made only of
+        # steady-state decode items is enqueued by one C++ call (see
+        # _native_step).  Needs lanes and either one stage or graph I/O.
+        self.native_exec = (self.device.type == "cuda" and bool(self.lanes)
+                            and os.environ.get("LSD_NATIVE_EXEC", "1") != "0"
+                            and (num_stages == 1 or self.graph_io))
+        self._ev_free: List[torch.cuda.Event] = []   # readout completion events
+        self._tev_free: List[torch.cuda.Event] = []  # busy-timing events
+        self._tev_used: List[torch.cuda.Event] = []
+        self.native_steps = 0
 
     # ------------------------------------------------------------------
     def configure(self, groups: int, cap: int) -> None:
@@ -329,6 +341,8 @@ class StageWorker:
     # timing
     def start_stats(self) -> None:
         self.stats = StepStats(self.device)
+        self._tev_free.extend(self._tev_used)
+        self._tev_used.clear()
 
     def end_stats(self) -> Optional[dict]:
         if self.stats is None:
@@ -372,12 +386,79 @@ class StageWorker:
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()
             self.step_events.append((plan.step, ev))
+        if self.native_exec:
+            if items and self._native_step(plan, items):
+                return
+            # the native path posts every receive in stream order itself: no
+            # look-ahead posting of the next step's first receive
+            following = []
         if items:
             self._post(items[0])
         for i, gp in enumerate(items):
             nx = items[i + 1] if i + 1 < len(items) else (following[0] if following else None)
             with self.on_lane(gp.g), trace_range(f"stage{self.r}/step{plan.step}/g{gp.g}"):
                 self._item(plan, gp, nx)
+
+    def _new_event(self, timing: bool) -> torch.cuda.Event:
+        """A created (recorded once) event whose raw handle C++ can record."""
+        pool = self._tev_free if timing else self._ev_free
+        if pool:
+            return pool.pop()
+        ev = torch.cuda.Event(enable_timing=timing)
+        ev.record(self.lanes[0])
+        return ev
+
+    def _native_step(self, plan: StepPlan, items: List[GroupPlan]) -> bool:
+        """Enqueue this step with one C++ call (csrc/stage_exec.cpp exec_items)
+        when every item is a steady-state decode item: a captured graph for
+        its (rows, context) bucket, no composition change, no prefill chunk,
+        no eager transfer (one stage, or graph I/O).  False = take the
+        Python item loop (nothing was issued)."""
+        if self.recv or any(self.send_pending.values()):
+            return False
+        descs = []
+        for gp in items:
+            if gp.kind == "fwd_b" or gp.chunks or gp.rows is not None or gp.b <= 0 or gp.n_final:
+                return False
+            io = self._io(gp)
+            if self.P > 1 and not io:
+                return False
+            gs = self.groups[gp.g]
+            ent = gs.graphs.get((gp.b, gp.ctxb, io))
+            if ent is None:
+                return False
+            ret = gp.ret if self.first else 0
+            if ret and (gs.tin.numel() < ret or (self.readout is not None and self.readout_native is None)):
+                return False
+            descs.append((gp, gs, ent[0], ret))
+        timing = plan.timing and self.stats is not None
+        C = self.stage.backend.C
+        rows, reads = [], []
+        for gp, gs, g, ret in descs:
+            lane = self.lanes[self.lane_of(gp.g)]
+            d = [0] * 12
+            d[0] = g.raw_cuda_graph_exec()
+            d[1] = lane.cuda_stream
+            if ret and self.P > 1:  # token-return receive from the last stage
+                h, me = self.t._edge("ret", self.P - 1, self.r, self.lane_of(gp.g))
+                d[2], d[3], d[4], d[5] = h, gs.tin.data_ptr(), 4 * ret, 1 - me
+            if timing:
+                t0, t1 = self._new_event(True), self._new_event(True)
+                self._tev_used += (t0, t1)
+                self.stats.marks.append((t0, t1))
+                d[6], d[11] = t0.cuda_event, t1.cuda_event
+            if ret and self.readout is not None:
+                host = torch.empty(ret, dtype=torch.int32, pin_memory=True)
+                ev = self._new_event(False)
+                d[7], d[8], d[9], d[10] = gs.tin.data_ptr(), host.data_ptr(), 4 * ret, ev.cuda_event
+                reads.append((gp, host, ev))
+            rows.append(d)
+        with self._gpu():
+            C.exec_items(rows)
+        for gp, host, ev in reads:
+            self.readout_native(plan, gp, host, ev, self._ev_free.append)
+        self.native_steps += 1
+        return True
 
     def _items(self, plan: Optional[StepPlan]) -> List[GroupPlan]:
         if plan is None or plan.end or plan.stop:

@@ -184,6 +184,8 @@ class Engine:
         self.scheduler = Scheduler(self, self.M, self.group_cap)
         if self.rank == 0:
             self.workers[0].readout = self.scheduler.on_readout
+            self.workers[0].readout_native = self.scheduler.on_readout_native
+            self.workers[0].readout_native = self.scheduler.on_readout_native
         for w in self.workers:
             w.use_graphs = cfg.use_graphs
             w.configure(self.M, self.group_cap)
@@ -318,6 +320,7 @@ class Engine:
             self.group_cap = -(-self.cfg.max_batch // self.M)
             self.scheduler = Scheduler(self, self.M, self.group_cap)
             self.workers[0].readout = self.scheduler.on_readout
+            self.workers[0].readout_native = self.scheduler.on_readout_native
             for w in self.workers:
                 w.configure(self.M, self.group_cap)
 

@@ -589,27 +589,46 @@ class Scheduler:
             def sync(ev=ev):
                 with GPU_GATE.shared():
                     ev.synchronize()
-            self.readouts.append((plan.step, ready, sync, host, key))
+            self.readouts.append((plan.step, ready, sync, host, key, None))
         else:
             host = ret[:n].clone()
-            self.readouts.append((plan.step, lambda: True, lambda: None, host, key))
+            self.readouts.append((plan.step, lambda: True, lambda: None, host, key, None))
+
+    def on_readout_native(self, plan: StepPlan, gp: GroupPlan, host: torch.Tensor, ev, release) -> None:
+        """Stage-0 native executor callback: the D2H copy of group gp.g's
+        previous token-return vector into `host` and its completion event
+        `ev` are already enqueued (csrc/stage_exec.cpp); `release(ev)` hands
+        the event back to the worker's pool once the readout is applied."""
+        from ..parallel.pipeline import GPU_GATE
+
+        def ready(ev=ev):
+            with GPU_GATE.shared():
+                return ev.query()
+
+        def sync(ev=ev):
+            with GPU_GATE.shared():
+                ev.synchronize()
+        self.readouts.append((plan.step, ready, sync, host, (plan.replica, plan.step, gp.g),
+                              lambda ev=ev: release(ev)))
 
     def push_remote_readout(self, step: int, tokens: List[int], prod_key) -> None:
         """Replica > 0 readouts arrive over the control plane (dist + DP)."""
         host = torch.tensor(tokens, dtype=torch.int32)
-        self.readouts.append((step, lambda: True, lambda: None, host, tuple(prod_key)))
+        self.readouts.append((step, lambda: True, lambda: None, host, tuple(prod_key), None))
 
     def poll(self, block_until_step: Optional[int] = None) -> None:
         """Process completed readouts (in order).  With block_until_step,
         wait for every readout of steps <= that one."""
         while self.readouts:
-            step, ready, sync, host, key = self.readouts[0]
+            step, ready, sync, host, key, release = self.readouts[0]
             if not ready():
                 if block_until_step is None or step > block_until_step:
                     return
                 sync()
             self.readouts.popleft()
             self._assign(host, key)
+            if release is not None:
+                release()
 
     def _assign(self, host: torch.Tensor, key) -> None:
         """Apply one group readout.  The core keeps every sequence's tokens

@@ -179,3 +179,26 @@ def test_join_running_batch_on_gpu():
     alone = _engine("gpt2-test")
     assert s_out == alone.generate_ids([[9, 8]], SamplingParams(greedy=True, max_new_tokens=3))[0]
     assert l_out == alone.generate_ids([[3, 4, 5]], sp_long)[0]
+
+
+@pytest.mark.parametrize("timing", [False, True])
+def test_native_stage_executor_matches_python_item_loop(monkeypatch, timing):
+    """Steady-state decode steps go through the native stage executor
+    (csrc/stage_exec.cpp: one C++ call per step -- graph launches, token
+    readout copies, busy-timing events) and give the Python item loop's tokens
+    bit for bit, with and without per-item timing events; EOS stops and
+    sequences leaving mid-session fall back to the Python loop for that step."""
+    prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 50)), [7] * 9, [3, 3]]
+    sps = [SamplingParams(temperature=0.8, top_k=20, seed=5, max_new_tokens=n) for n in (12, 5, 16, 9, 1)]
+    monkeypatch.setenv("LSD_NATIVE_EXEC", "0")
+    py = _engine("gpt2-test", num_microbatches=2)
+    want = py.generate_ids(prompts, sps, record_timing=timing)
+    assert sum(w.native_steps for w in py.workers) == 0
+    monkeypatch.setenv("LSD_NATIVE_EXEC", "1")
+    nat = _engine("gpt2-test", num_microbatches=2)
+    assert nat.generate_ids(prompts, sps, record_timing=timing) == want
+    got = nat.generate_ids(prompts, sps, record_timing=timing)  # graphs cached: native steps
+    assert got == want
+    assert sum(w.native_steps for w in nat.workers) > 0
+    if timing:
+        assert nat.last_session is not None and 0.0 < nat.last_session.stages[0]["busy_fraction"] <= 1.0
