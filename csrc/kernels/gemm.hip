@@ -510,11 +510,33 @@ typedef __attribute__((address_space(1))) const void gbl_cvoid;
 // the 16-B chunk index XOR-swizzled by (row>>1)&7.  glds writes lane-linear
 // (base + 16*lane), so the swizzle goes on the per-lane SOURCE address and the
 // same XOR is applied on the read (guide §5.4 rule 21).
-template <int ROWS = TBM>
+// kStageBL: the 4- and 8-wave decode / tiled stagers (stage_tile, stage8) issue buffer_load ...
+// lds from a wave-uniform resource at (row0, k0) with 32-bit lane offsets instead of
+// global_load_lds with 64-bit lane addresses (-DLSD_GLDS_GLOBAL restores the latter for A/B).
+#ifdef LSD_GLDS_GLOBAL
+constexpr bool kStageBL = false;
+#else
+constexpr bool kStageBL = false;
+#endif
+
+template <int ROWS = TBM, bool BL = kStageBL>
 __device__ __forceinline__ void stage_tile(char* lds_tile, const bf16* src, long ld, int row0,
                                            int row_max, int k0) {
   const int lane = lane_id(), w = threadIdx.x >> 6;
   constexpr int PER_WAVE = ROWS / 32;  // wave-instructions of 1 KiB (8 rows of 64 k) per wave
+  if constexpr (BL) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(src + (long)row0 * ld + k0), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < PER_WAVE; ++q) {
+      const int inst = w * PER_WAVE + q;
+      const int row = inst * 8 + (lane >> 3);
+      const int lch = (lane & 7) ^ ((row >> 1) & 7);
+      const int off = ((min(row0 + row, row_max) - row0) * (int)ld + lch * 8) * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds_tile + inst * 1024), 16, off, 0, 0, 0);
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < PER_WAVE; ++q) {
     const int inst = w * PER_WAVE + q;
@@ -736,12 +758,28 @@ __global__ __launch_bounds__(256) void gemm_ring_kernel(GemmParams p, int tiles_
 
 // Stage a [ROWS][64 k] tile (the lds_frag image) with NWAVES waves sharing
 // the ROWS / 8 wave-instructions; `wi` = this wave's index among them.
-template <int ROWS, int NWAVES, int AUX = 0>
+// BL: buffer_load ... lds from a wave-uniform resource at (row0, k0) with 32-bit lane
+// offsets instead of global_load_lds with 64-bit lane addresses (fewer issue cycles
+// per DMA instruction: prefill GEMM +6-25 %, profiles/r3_p8_buffer_lds.log).
+template <int ROWS, int NWAVES, int AUX = 0, bool BL = false>
 __device__ __forceinline__ void stage_rows(char* lds_tile, const bf16* src, long ld, int row0, int row_max,
                                            int k0, int wi) {
   const int lane = lane_id();
   constexpr int PER_WAVE = ROWS / 8 / NWAVES;
   static_assert(PER_WAVE * 8 * NWAVES == ROWS, "rows split evenly over the loading waves");
+  if constexpr (BL) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(src + (long)row0 * ld + k0), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < PER_WAVE; ++q) {
+      const int inst = wi * PER_WAVE + q;
+      const int row = inst * 8 + (lane >> 3);
+      const int lch = (lane & 7) ^ ((row >> 1) & 7);
+      const int off = ((min(row0 + row, row_max) - row0) * (int)ld + lch * 8) * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds_tile + inst * 1024), 16, off, 0, 0, AUX);
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < PER_WAVE; ++q) {
     const int inst = wi * PER_WAVE + q;
@@ -800,7 +838,7 @@ __device__ __forceinline__ void stage_rows_packed(char* lds_tile, const bf16* sr
 // reloads the other partials (sc1 loads) and sums all S in split order
 // (deterministic) before the fused epilogue (guide §5 "In-launch split-K
 // reduction", sc1 form: no release / acquire fences).
-template <int EPI, int VAR, int SLOTS, int NTW = 0, int PK = 0>
+template <int EPI, int VAR, int SLOTS, int NTW = 0, int PK = 0, bool BL = kStageBL>
 __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles_m, int tiles_n, int rot,
                                                          int* __restrict__ cnt, float* __restrict__ ws) {
   constexpr int D = SLOTS - 1, TN = 64, TM = TBM;
@@ -845,9 +883,9 @@ __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles
     int k = kt - kb + r0;
     k = kb + (k >= nk ? k - nk : k);
     if constexpr (PK & 2) stage_rows_packed<TM, LWN, 0>(b, p.A, p.M, p.K / 64, m0, p.M - 1, k, lw);
-    else stage_rows<TM, LWN>(b, p.A, p.lda, m0, p.M - 1, k * TBK, lw);
+    else stage_rows<TM, LWN, 0, BL>(b, p.A, p.lda, m0, p.M - 1, k * TBK, lw);
     if constexpr (PK & 1) stage_rows_packed<TN, LWN, 1>(b + A_BYTES, p.W, p.N, p.K / 64, n0, p.N - 1, k, lw);
-    else stage_rows<TN, LWN, NTW ? 2 : 0>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, k * TBK, lw);
+    else stage_rows<TN, LWN, NTW ? 2 : 0, BL>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, k * TBK, lw);
   };
   if (loader) {
 #pragma unroll
@@ -1222,9 +1260,25 @@ constexpr int P8_HALF = 128 * 64 * 2;  // 16 KiB
 constexpr int P8_BUF = 4 * P8_HALF;    // A0 A1 B0 B1
 constexpr int P8_SMEM = 2 * P8_BUF;    // 128 KiB (== 256 x 128 fp32 C half-tile)
 
+template <bool BUF = false>
 __device__ __forceinline__ void p8_stage(char* lds, const bf16* src, long ld, int row0, int row_max,
                                          int k0) {
   const int lane = lane_id(), w = threadIdx.x >> 6;
+  if constexpr (BUF) {
+    // buffer_load ... lds: a wave-uniform resource at (row0, k0) and 32-bit lane offsets
+    // (one address VGPR per lane instead of a 64-bit global address)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(src + (long)row0 * ld + k0), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int inst = w * 2 + q;
+      const int row = inst * 8 + (lane >> 3);
+      const int lch = (lane & 7) ^ ((row >> 1) & 7);
+      const int off = ((min(row0 + row, row_max) - row0) * (int)ld + lch * 8) * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + inst * 1024), 16, off, 0, 0, 0);
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int inst = w * 2 + q;  // 16 x 1 KiB = 128 rows of 128 B
@@ -1235,7 +1289,11 @@ __device__ __forceinline__ void p8_stage(char* lds, const bf16* src, long ld, in
   }
 }
 
-template <int EPI>
+// VAR (A/B, gemm_set_big_kind 2/3): bit 0 issues each phase's LDS-DMA before its
+// fragment reads (p8 loop stamps: a glds issued behind 12 ds_read_b128 costs the wave
+// 100+ cycles); bit 1 reads q0's B fragments before its A fragments; bit 2 stages
+// with buffer_load ... lds (32-bit lane offsets) instead of global_load_lds.
+template <int EPI, int VAR = 0>
 __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
   __shared__ __attribute__((aligned(16))) char smem[P8_SMEM];
   const int nwg = gridDim.x;
@@ -1264,8 +1322,8 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
   auto stage = [&](int t, int h) {
     char* dst = smem + (t & 1) * P8_BUF + h * P8_HALF;
     const int k0 = (kb + t) * 64;
-    if (h < 2) p8_stage(dst, p.A, p.lda, m0 + h * 128, p.M - 1, k0);
-    else p8_stage(dst, p.W, p.ldw, n0 + (h - 2) * 128, p.N - 1, k0);
+    if (h < 2) p8_stage<(VAR & 4) != 0>(dst, p.A, p.lda, m0 + h * 128, p.M - 1, k0);
+    else p8_stage<(VAR & 4) != 0>(dst, p.W, p.ldw, n0 + (h - 2) * 128, p.N - 1, k0);
   };
   bf16x8 af[4][2], b0[2][2], b1[2][2];
   auto read_a = [&](int t, int mh) {
@@ -1331,21 +1389,45 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
     for (int t = 0; t < T; ++t) {
       const bool n1 = t + 1 < T, n2 = t + 2 < T;
       // q0: (A0, B0)
-      read_a(t, 0);
-      read_b(t, 0, b0);
-      if (n1) stage(t + 1, 3);
+      if constexpr ((VAR & 1) != 0) {
+        if (n1) stage(t + 1, 3);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr ((VAR & 2) != 0) {
+        read_b(t, 0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(t, 0);
+      } else {
+        read_a(t, 0);
+        read_b(t, 0, b0);
+      }
+      if constexpr ((VAR & 1) == 0) {
+        if (n1) stage(t + 1, 3);
+      }
       __builtin_amdgcn_sched_barrier(0);
       mma(0, 0, b0);
       // q1: (A0, B1); retire A1(t): 4 later halves in flight when t + 1 exists
-      read_b(t, 1, b1);
-      if (n1) stage(t + 1, 1);
+      if constexpr ((VAR & 1) != 0) {
+        if (n1) stage(t + 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        read_b(t, 1, b1);
+      } else {
+        read_b(t, 1, b1);
+        if (n1) stage(t + 1, 1);
+      }
       P8_ACC(pf_vm, if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
                     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory"))
       __builtin_amdgcn_sched_barrier(0);
       mma(0, 1, b1);
       // q2: (A1, B1)
-      read_a(t, 1);
-      if (n2) stage(t + 2, 0);
+      if constexpr ((VAR & 1) != 0) {
+        if (n2) stage(t + 2, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(t, 1);
+      } else {
+        read_a(t, 1);
+        if (n2) stage(t + 2, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       mma(1, 1, b1);
       // q3: (A1, B0); retire A0 / B0 / B1 of t + 1 (A1(t+1), A0 / B0(t+2) stay in flight)
@@ -1440,21 +1522,12 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
 //     the last-arriving split sums the S partials in split order
 //     (deterministic) and runs the fused epilogue.  A tile's splits have
 //     consecutive remapped ids, so they share an XCD (speed only).
-template <int ROWS>
+template <int ROWS, bool BL = kStageBL>
 __device__ __forceinline__ void stage8(char* lds_tile, const bf16* src, long ld, int row0, int row_max,
                                        int k0) {
   // 8 waves: ROWS / 64 wave-instructions of 1 KiB (8 rows x 128 B) each, the
   // [ROWS][64 k] image with 16-B chunks swizzled by (row >> 1) & 7 (lds_frag)
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  constexpr int PER_WAVE = ROWS / 64;
-#pragma unroll
-  for (int q = 0; q < PER_WAVE; ++q) {
-    const int inst = w * PER_WAVE + q;
-    const int row = inst * 8 + (lane >> 3);
-    const int lch = (lane & 7) ^ ((row >> 1) & 7);
-    const bf16* gp = src + (long)min(row0 + row, row_max) * ld + k0 + lch * 8;
-    __builtin_amdgcn_global_load_lds((gbl_cvoid*)gp, (lds_void*)(lds_tile + inst * 1024), 16, 0, 0);
-  }
+  stage_rows<ROWS, 8, 0, BL>(lds_tile, src, ld, row0, row_max, k0, threadIdx.x >> 6);
 }
 
 template <int BN, int SLOTS>
@@ -1635,8 +1708,10 @@ static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
 // GEMMs 10-25 % faster than M-fastest, 8 equal, 16+ slower
 // (profiles/r2_prefill_tile_order.log)
 static int g_big_group = 4;
-// lsd_gemm_set_big_kind(): 0 = BK=32 ring kernel (gemm_big), 1 = phase-pipelined BK=64 (gemm_p8)
-static int g_big_kind = 1;
+// lsd_gemm_set_big_kind(): 0 = BK=32 ring kernel (gemm_big), 1 = phase-pipelined BK=64 (gemm_p8),
+// 2..5 = gemm_p8 VAR 1..5 (4, the default: buffer_load ... lds staging, +6 % on the GPT-2 XL prefill
+// projections and +25 % at 4096^3 over kind 1; profiles/r3_p8_buffer_lds.log)
+static int g_big_kind = 4;
 // 128x128 launches of at most this many workgroups use the 3-slot ring kernel
 // (1 block/CU); larger grids keep the 2-blocks/CU double-buffered one.
 // lsd_gemm_set_tiled3_max(): tuning / tests; 0 = off
@@ -1751,6 +1826,18 @@ static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStre
     if (g_big_kind == 1)
       hipLaunchKernelGGL((gemm_p8_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
                          g_big_group);
+    else if (g_big_kind == 2)
+      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 1>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+                         g_big_group);
+    else if (g_big_kind == 3)
+      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 3>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+                         g_big_group);
+    else if (g_big_kind == 4)
+      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 4>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+                         g_big_group);
+    else if (g_big_kind == 5)
+      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 5>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+                         g_big_group);
     else
       hipLaunchKernelGGL((gemm_big_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
                          g_big_group);
@@ -1797,6 +1884,8 @@ static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStre
         hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 2>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else if (g_ring8 == 2 && g_ring8_pack == 3)
         hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 3>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
+      else if (g_ring8 == 2 && (g_ring8_flags & 4))
+        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 0, true>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else if (g_ring8 == 2 && (g_ring8_flags & 2))
         hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 1>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else if (g_ring8 == 2)
@@ -1827,14 +1916,14 @@ using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
 extern "C" void lsd_gemm_set_big_group(int v) { g_big_group = v < 0 ? 0 : v; }
-extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = v == 1 ? 1 : 0; }
+extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v >= 0 && v <= 5) ? v : 0; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }
 extern "C" void lsd_gemm_set_ring_fill(int v) { g_ring_fill = v; }
 extern "C" void lsd_gemm_set_ring_m96(int v) { g_ring_m96 = v; }
 extern "C" void lsd_gemm_set_ring8(int v) { g_ring8 = (v == 1 || v == 2) ? v : 0; }
-extern "C" void lsd_gemm_set_ring8_flags(int v) { g_ring8_flags = v & 3; }
+extern "C" void lsd_gemm_set_ring8_flags(int v) { g_ring8_flags = v & 7; }
 extern "C" void lsd_gemm_set_ring8_pack(int v) { g_ring8_pack = v & 3; }
 extern "C" void lsd_gemm_set_d256_slots(int v) { g_d256_slots = v < 2 ? 2 : (v > 4 ? 4 : v); }
 // columns per gemm_d256 tile of a launch of this kind (0: not a d256 launch):

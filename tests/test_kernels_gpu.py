@@ -337,14 +337,23 @@ def BIG(C):
     C.gemm_set_big_min(160)
 
 
+@pytest.fixture(params=[4, 1, 0])
+def BIGK(BIG, request):
+    """The 256x256 kernel kinds: 4 = phase-pipelined BK=64 with buffer_load ... lds staging
+    (default), 1 = the same with global_load_lds, 0 = the BK=32 4-slot ring."""
+    BIG.gemm_set_big_kind(request.param)
+    yield BIG
+    BIG.gemm_set_big_kind(4)
+
+
 @pytest.mark.parametrize("M", [256, 300, 777, 1300])
 @pytest.mark.parametrize("K", [64, 128, 384])
-def test_big_gemm_epilogues(BIG, CNT, M, K):
+def test_big_gemm_epilogues(BIGK, CNT, M, K):
     """256x256 ring-pipelined kernel: every epilogue, M/N tails, K of 2, 4 and 12
     k-steps (fewer than, equal to and more than the ring depth)."""
     from llm_sharding_demo_amd.ops.hip import interleave_gate_up
 
-    C = BIG
+    C = BIGK
     N = 320  # second column tile is a 64-wide tail
     a, w, bias = bf(M, K, seed=40), bf(N, K, scale=0.05, seed=41), bf(N, scale=0.1, seed=42)
     y_ref = ref.linear(a, w, bias)

@@ -655,6 +655,9 @@ def main():
     if "p8stamps" in which:
         stamps_p8()
         stamps_p8(N=1600, K=6400, act=0)
+    if "p8prof" in which:  # LSD_P8_PROF build: loop cycles split into vmcnt waits and the two barriers
+        stamps_p8(act=0)
+        stamps_p8(M=4096, N=4096, K=4096, act=0)
     if "lmk" in which:
         for M in (256, 512):
             bench_lmhead_kinds(M)
