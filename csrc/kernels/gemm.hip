@@ -1498,6 +1498,210 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
 }
 
 // ---------------------------------------------------------------------------
+// Persistent prefill GEMM (kind 6): the p8 k-loop as one stream across tiles
+// ---------------------------------------------------------------------------
+// gridDim.x (a multiple of 8, <= the CU count) workgroups; workgroup b runs the
+// tiles b, b + gridDim.x, ... in the launch-per-tile kernel's XCD-aware order
+// (xcd_remap of the virtual block id keeps every tile on the XCD it had there).
+// Its tiles' 64-deep k-tiles form ONE stream u = 0 .. ntiles * T - 1 and the p8
+// half-tile DMA schedule (q0 B1(u+1), q1 A1(u+1), q2 A0(u+2), q3 B0(u+2)) runs on
+// across tile boundaries, so the next tile's first k-tile and a half are in
+// flight while a tile's epilogue runs, and no workgroup pays a launch, a
+// prologue or a cold pipeline per tile (p8 stamps: prologue 1.7 us + epilogue
+// 8-12 us of a 62 us K = 1600 block, profiles/r2_p8_stamps_lmhead.log).
+// The epilogue stages C through 32 KiB of LDS of its own (8 passes of 64 rows
+// x 128 columns: every wave contributes a 32 x 32 block per pass), outside the
+// 128 KiB operand ring, with raw s_barriers behind lgkmcnt(0) waits only: the
+// operand DMA in flight is never drained by it.  Its global loads / stores are
+// younger than every staged half-tile, so the counted vmcnt waits of the next
+// k-tiles still retire what they retired (they may wait longer, never less).
+// The wave-row stagger is undone before an epilogue and redone after it.
+// splits == 1 only (one k-range per tile).  A/B only (gemm_set_big_kind(6)): measured 8-18 %
+// slower than kind 4, profiles/r3_rejected_persistent_prefill_gemm.log (compiler-inserted vmcnt(0)
+// before the epilogue's global loads also wait for the previous pass's stores).
+constexpr int PP_CT_BYTES = 64 * 128 * 4;        // 32 KiB fp32 C slice
+constexpr int PP_SMEM = P8_SMEM + PP_CT_BYTES;   // 160 KiB
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
+  __shared__ __attribute__((aligned(16))) char smem[PP_SMEM];
+  const int total = tiles_m * tiles_n;
+  const int nb = (int)gridDim.x, b0 = (int)blockIdx.x;
+  const int ntile = (total - b0 + nb - 1) / nb;
+  const int T = p.K / 64;
+  const int U = ntile * T;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int r = lane & 15, g = lane >> 4;
+
+  auto tile_of = [&](int j, int& m0, int& n0) {
+    int tm, tn;
+    tile_order(xcd_remap(b0 + j * nb, total), tiles_m, tiles_n, G, tm, tn);
+    m0 = tm * 256;
+    n0 = tn * 256;
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // half h (0 = A0, 1 = A1, 2 = B0, 3 = B1) of the k-tile at k0 of the tile at
+  // (m0, n0) into LDS buffer `buf`; the stream position is tracked by the loop
+  // (current tile, next tile, k-tile index) instead of dividing u by T per call
+  auto stage = [&](int buf, int m0, int n0, int k0, int h) {
+    char* dst = smem + buf * P8_BUF + h * P8_HALF;
+    if (h < 2) p8_stage<true>(dst, p.A, p.lda, m0 + h * 128, p.M - 1, k0);
+    else p8_stage<true>(dst, p.W, p.ldw, n0 + (h - 2) * 128, p.N - 1, k0);
+  };
+  bf16x8 af[4][2], b0f[2][2], b1f[2][2];
+  auto read_a = [&](int u, int mh) {
+    const char* src = smem + (u & 1) * P8_BUF + mh * P8_HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = lds_frag(src, wr * 64 + i * 16 + r, kk * 4 + g);
+  };
+  auto read_b = [&](int u, int nh, bf16x8 (&bf)[2][2]) {
+    const char* src = smem + (u & 1) * P8_BUF + (2 + nh) * P8_HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = lds_frag(src, wc * 32 + j * 16 + r, kk * 4 + g);
+  };
+  auto mma = [&](int mh, int nh, bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_waitcnt(LGKM0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh * 4 + i][nh * 2 + j] = mfma16(af[i][kk], bf[j][kk], acc[mh * 4 + i][nh * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  float* ct = reinterpret_cast<float*>(smem + P8_SMEM);
+  auto epilogue = [&](int m0, int n0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int mh = e >> 2, nh = (e >> 1) & 1, i2 = e & 1;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = wr * 32 + ii * 16 + 4 * g + q;
+            const int col = wc * 32 + jj * 16 + r;
+            ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[mh * 4 + i2 * 2 + ii][nh * 2 + jj][q];
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int c0 = 0; c0 < 2; ++c0) {
+        const int c = (int)threadIdx.x + c0 * 512;
+        const int row = c >> 4, ch = c & 15;
+        const int m = m0 + mh * 128 + (row >> 5) * 64 + i2 * 32 + (row & 31);
+        const int n = n0 + nh * 128 + ch * 8;
+        if (m >= p.M || n >= p.N) continue;
+        const float* src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if constexpr (EPI == EPI_SILU_MUL) {
+          if ((ch & 3) >= 2) continue;  // up chunks are read by their gate chunk
+          const float* up = ct + row * 128 + (((ch + 2) * 8) ^ (((row >> 2) & 3) << 4));
+          const f32x4 ulo = *reinterpret_cast<const f32x4*>(up);
+          const f32x4 uhi = *reinterpret_cast<const f32x4*>(up + 4);
+          const float uu[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+          bf16x8 o;
+#pragma unroll
+          for (int x = 0; x < 8; ++x) o[x] = f2bf(silu(v[x]) * uu[x]);
+          st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
+        } else {
+          epilogue8<EPI>(p, m, n, v, 0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // slice read before the next pass overwrites it
+    }
+  };
+
+  if (U > 0) {
+    int cm0, cn0, xm0 = 0, xn0 = 0;  // current tile, next tile
+    tile_of(0, cm0, cn0);
+    if (ntile > 1) tile_of(1, xm0, xn0);
+    stage(0, cm0, cn0, 0, 0);
+    stage(0, cm0, cn0, 0, 2);
+    stage(0, cm0, cn0, 0, 3);
+    stage(0, cm0, cn0, 0, 1);
+    if (U > 1) {  // k-tile 1 of the stream: this tile's (T >= 2: host-checked)
+      stage(1, cm0, cn0, 64, 0);
+      stage(1, cm0, cn0, 64, 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+
+    int kt = 0, j = 0;
+    for (int t = 0; t < U; ++t) {
+      const bool n1 = t + 1 < U, n2 = t + 2 < U;
+      // stream k-tiles t + 1 and t + 2: (tile, k0)
+      const bool s1 = kt + 1 < T, s2 = kt + 2 < T;
+      const int m1 = s1 ? cm0 : xm0, c1 = s1 ? cn0 : xn0, k1 = s1 ? (kt + 1) * 64 : 0;
+      const int m2 = s2 ? cm0 : xm0, c2 = s2 ? cn0 : xn0, k2 = s2 ? (kt + 2) * 64 : (kt + 2 - T) * 64;
+      const int bq = (t + 1) & 1, bt = t & 1;
+      // q0: (A0, B0)
+      read_a(t, 0);
+      read_b(t, 0, b0f);
+      if (n1) stage(bq, m1, c1, k1, 3);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0, 0, b0f);
+      // q1: (A0, B1); retire A1(t)
+      read_b(t, 1, b1f);
+      if (n1) stage(bq, m1, c1, k1, 1);
+      if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0, 1, b1f);
+      // q2: (A1, B1)
+      read_a(t, 1);
+      if (n2) stage(bt, m2, c2, k2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1, 1, b1f);
+      // q3: (A1, B0); retire A0 / B0 / B1 of t + 1
+      if (n2) stage(bt, m2, c2, k2, 2);
+      if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (n1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1, 0, b0f);
+      if (++kt == T) {  // tile j done: de-stagger, epilogue, re-stagger
+        if (wr == 0) __builtin_amdgcn_s_barrier();
+        epilogue(cm0, cn0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (wr == 1 && n1) __builtin_amdgcn_s_barrier();
+        kt = 0;
+        ++j;
+        cm0 = xm0;
+        cn0 = xn0;
+        if (j + 1 < ntile) tile_of(j + 1, xm0, xn0);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Decode GEMM at 129-256 rows: every row in ONE 256 x BN tile, 8 waves
 // ---------------------------------------------------------------------------
 // The 128x64 ring tiles above read the whole A operand once per column tile
@@ -1817,6 +2021,20 @@ static hipError_t launch_d256(const GemmParams& p, int kind, int* cnt, float* ws
   return bn == 128 ? launch_d256_bn<EPI, 128>(p, cnt, ws, st) : launch_d256_bn<EPI, 64>(p, cnt, ws, st);
 }
 
+// persistent prefill GEMM grid: the CU count rounded down to a multiple of 8
+// (every workgroup keeps one XCD), 1 workgroup per CU (160 KiB LDS)
+static int pp_grid() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8)
+      cus = 256;
+    n = cus / 8 * 8;
+  }
+  return n;
+}
+
 template <int EPI>
 static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
   // 256x256 pipelined kernel once the problem fills the chip with 1-block/CU
@@ -1837,6 +2055,11 @@ static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStre
                          g_big_group);
     else if (g_big_kind == 5)
       hipLaunchKernelGGL((gemm_p8_kernel<EPI, 5>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+                         g_big_group);
+    else if (g_big_kind == 6 && p.splits == 1 && p.K >= 128 && bm * bn >= pp_grid())
+      hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(pp_grid()), dim3(512), 0, st, p, bm, bn, g_big_group);
+    else if (g_big_kind == 6)
+      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 4>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
                          g_big_group);
     else
       hipLaunchKernelGGL((gemm_big_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
@@ -1916,7 +2139,7 @@ using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
 extern "C" void lsd_gemm_set_big_group(int v) { g_big_group = v < 0 ? 0 : v; }
-extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v >= 0 && v <= 5) ? v : 0; }
+extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v >= 0 && v <= 6) ? v : 0; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }
