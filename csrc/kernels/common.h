@@ -122,6 +122,44 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Mean / variance statistics (count, mean, M2 = sum of squared deviations),
+// merged with Chan's pairwise formula in a form symmetric in its two operands
+// (m = (na ma + nb mb) / n), so both lanes of a butterfly pair -- and every
+// thread of a block -- end with bit-identical results.
+struct Wf {
+  float n, m, M;
+};
+__device__ __forceinline__ Wf wf_merge(Wf a, Wf b) {
+  const float n = a.n + b.n;
+  if (n == 0.f) return a;
+  const float d = b.m - a.m, rn = 1.f / n;
+  return {n, (a.n * a.m + b.n * b.m) * rn, a.M + b.M + d * d * (a.n * b.n) * rn};
+}
+template <int OFF>
+__device__ __forceinline__ Wf wf_xchg(Wf v) {
+  return {wave_xchg<OFF>(v.n), wave_xchg<OFF>(v.m), wave_xchg<OFF>(v.M)};
+}
+// Block-wide merge in ONE LDS round (red: >= 3 x waves floats)
+__device__ __forceinline__ Wf block_welford(Wf v, float* red) {
+  v = wf_merge(v, wf_xchg<1>(v));
+  v = wf_merge(v, wf_xchg<2>(v));
+  v = wf_merge(v, wf_xchg<4>(v));
+  v = wf_merge(v, wf_xchg<8>(v));
+  v = wf_merge(v, wf_xchg<16>(v));
+  v = wf_merge(v, wf_xchg<32>(v));
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane_id() == 0) {
+    red[3 * w] = v.n;
+    red[3 * w + 1] = v.m;
+    red[3 * w + 2] = v.M;
+  }
+  __syncthreads();
+  Wf t = {red[0], red[1], red[2]};
+  for (int i = 1; i < nw; ++i) t = wf_merge(t, Wf{red[3 * i], red[3 * i + 1], red[3 * i + 2]});
+  return t;
+}
+
 // Block-wide sum for blockDim.x = nwaves*64 (<= 1024); `red` holds >= 16 floats.
 __device__ __forceinline__ float block_sum(float v, float* red) {
   v = wave_sum(v);

@@ -126,9 +126,55 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int row0, int n, 
 // Row-contiguous epilogue of 8 consecutive columns [n, n+8) of row m (the
 // tiled kernel's LDS-transposed output): every store is one 16-byte vector.
 // n % 8 == 0; bias / out / x / caches are 16-byte aligned (host-checked).
+//
+// Split in three so a store pass can issue the global reads of ALL its chunks
+// before its first store (store_pass below): CDNA4's vmcnt counts loads and
+// stores in one in-order counter, so a load issued after a store is waited for
+// together with that store, and a chunk-at-a-time loop (load bias / residual,
+// wait, compute, store) serialises one store round trip per chunk (the p8
+// epilogue: 16 per thread, most of its 6-12 us).
+//   epi8_pre  -- bias, residual x, QKV position / slot      (independent loads)
+//   epi8_pre2 -- QKV RoPE (cos, sin) of that position        (dependent loads)
+//   epi8_post -- the math and the stores
+// s_waitcnt immediate for vmcnt(n) alone (gfx9 layout: vmcnt[3:0] | vmcnt[5:4] << 14)
+constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+
+struct Epi8Pre {
+  bf16x8 b;
+  f32x4 x0, x1, cs0, cs1;
+  int pos, slot;
+};
+
 template <int EPI>
-__device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v,
-                                          int split) {
+__device__ __forceinline__ void epi8_pre(const GemmParams& p, int m, int n, Epi8Pre& e) {
+  if constexpr (EPI == EPI_SLAB || EPI == EPI_F32 || EPI == EPI_SILU_MUL) return;
+  if (p.bias) e.b = ld8(p.bias + n);
+  if constexpr (EPI == EPI_RESID) {
+    const f32x4* x = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.out) + (long)m * p.ldo + n);
+    e.x0 = x[0];
+    e.x1 = x[1];
+  }
+  if constexpr (EPI == EPI_QKV) {
+    e.pos = p.tpos[m];
+    e.slot = n >= p.q_size ? p.tslot[m] : 0;
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epi8_pre2(const GemmParams& p, int n, Epi8Pre& e) {
+  if constexpr (EPI == EPI_QKV) {
+    if (p.rope != nullptr && n < p.q_size + p.kv_size) {
+      const int d0 = (n < p.q_size ? n : n - p.q_size) % p.hd;
+      const f32x4* cs = reinterpret_cast<const f32x4*>(p.rope + ((long)e.pos * (p.hd >> 1) + (d0 >> 1)) * 2);
+      e.cs0 = cs[0];
+      e.cs1 = cs[1];
+    }
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epi8_post(const GemmParams& p, int m, int n, const float* v, int split,
+                                          const Epi8Pre& e) {
   if constexpr (EPI == EPI_SLAB || EPI == EPI_F32) {
     float* o = EPI == EPI_SLAB ? p.slab + (long)split * p.M * p.N + (long)m * p.N + n
                                : reinterpret_cast<float*>(p.out) + (long)m * p.ldo + n;
@@ -138,16 +184,15 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
   }
   float y[8];
   if (p.bias) {
-    const bf16x8 b = ld8(p.bias + n);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) y[j] = v[j] + bf2f(b[j]);
+    for (int j = 0; j < 8; ++j) y[j] = v[j] + bf2f(e.b[j]);
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) y[j] = v[j];
   }
   if constexpr (EPI == EPI_RESID) {
     f32x4* x = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out) + (long)m * p.ldo + n);
-    f32x4 x0 = x[0], x1 = x[1];
+    f32x4 x0 = e.x0, x1 = e.x1;
 #pragma unroll
     for (int j = 0; j < 4; ++j) { x0[j] += y[j]; x1[j] += y[4 + j]; }
     x[0] = x0;
@@ -163,19 +208,16 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
   }
   if constexpr (EPI == EPI_QKV) {
     const int qk = p.q_size + p.kv_size;
-    const int pos = p.tpos[m];
     if (p.rope != nullptr && n < qk) {  // adjacent (even, odd) pairs rotate together
-      const int d0 = (n < p.q_size ? n : n - p.q_size) % p.hd;
-      const f32x4* cs = reinterpret_cast<const f32x4*>(p.rope + ((long)pos * (p.hd >> 1) + (d0 >> 1)) * 2);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f32x4 t = cs[h];  // (cos, sin) of pairs d0/2 + 2h, d0/2 + 2h + 1
+        const f32x4 t = h ? e.cs1 : e.cs0;  // (cos, sin) of pairs d0/2 + 2h, d0/2 + 2h + 1
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const float c = t[2 * e], s = t[2 * e + 1];
-          const float a = y[4 * h + 2 * e], b = y[4 * h + 2 * e + 1];
-          y[4 * h + 2 * e] = a * c - b * s;
-          y[4 * h + 2 * e + 1] = b * c + a * s;
+        for (int q = 0; q < 2; ++q) {
+          const float c = t[2 * q], sn = t[2 * q + 1];
+          const float a = y[4 * h + 2 * q], b = y[4 * h + 2 * q + 1];
+          y[4 * h + 2 * q] = a * c - b * sn;
+          y[4 * h + 2 * q + 1] = b * c + a * sn;
         }
       }
     }
@@ -187,8 +229,54 @@ __device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, con
     } else {
       const int c = n < qk ? n - p.q_size : n - qk;
       bf16* cache = n < qk ? p.kc : p.vc;
-      st8(cache + (((long)p.tslot[m] * p.n_kv + c / p.hd) * p.max_seq + pos) * p.hd + c % p.hd, o);
+      st8(cache + (((long)e.slot * p.n_kv + c / p.hd) * p.max_seq + e.pos) * p.hd + c % p.hd, o);
     }
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue8(const GemmParams& p, int m, int n, const float* v, int split) {
+  Epi8Pre e;
+  epi8_pre<EPI>(p, m, n, e);
+  epi8_pre2<EPI>(p, n, e);
+  epi8_post<EPI>(p, m, n, v, split, e);
+}
+
+// One store pass over the 8-column row chunks c = threadIdx.x + i * NT (i < NCH,
+// c < nchunks) of an fp32 C image in LDS.  at(c, m, n, src) maps a chunk to its
+// output row / column and its 8 floats in LDS (false: out of range).  Every
+// global read of the thread's chunks is issued before its first store (see
+// epi8_pre); SiLU·up pairs each gate chunk with the up chunk 16 columns right
+// (interleaved [gate16 | up16] 32-column blocks in one tile: `up` = src + UPOFF).
+template <int EPI, int NCH, int NT, class At>
+__device__ __forceinline__ void store_pass(const GemmParams& p, int nchunks, int split, At at) {
+  Epi8Pre e[NCH];
+  int mm[NCH], nn[NCH];
+  const float* sp[NCH];
+  bool ok[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = (int)threadIdx.x + i * NT;
+    ok[i] = c < nchunks && at(c, mm[i], nn[i], sp[i]);
+    if (ok[i]) epi8_pre<EPI>(p, mm[i], nn[i], e[i]);
+  }
+  // one explicit wait for all of them: the compiler's own waits after the
+  // branchy chunk bodies below would be vmcnt(0) per chunk (joins lose count),
+  // i.e. one store round trip per chunk again
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  if constexpr (EPI == EPI_QKV) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      if (ok[i]) epi8_pre2<EPI>(p, nn[i], e[i]);
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  }
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    if (!ok[i]) continue;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(sp[i]);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(sp[i] + 4);
+    const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    epi8_post<EPI>(p, mm[i], nn[i], v, split, e[i]);
   }
 }
 
@@ -472,11 +560,14 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmParams p, int* __restr
           ct[(mt * 16 + 4 * g + q) * CLD + w * 16 * NW + ns * 16 + r] = acc[mt][ns][q];
     __syncthreads();
     const int n0 = tile * BNB;
-    for (int c = threadIdx.x; c < ROWS * (BNB / 8); c += 256) {
-      const int row = c / (BNB / 8), ch = c % (BNB / 8);
-      const int m = rb0 + row, n = n0 + ch * 8;
-      if (m < p.M && n < p.N) epilogue8<EPI>(p, m, n, ct + row * CLD + ch * 8, split);
-    }
+    store_pass<EPI, (ROWS * (BNB / 8) + 255) / 256, 256>(
+        p, ROWS * (BNB / 8), split, [&](int c, int& m, int& n, const float*& src) {
+          const int row = c / (BNB / 8), ch = c % (BNB / 8);
+          m = rb0 + row;
+          n = n0 + ch * 8;
+          src = ct + row * CLD + ch * 8;
+          return m < p.M && n < p.N;
+        });
   } else {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -560,6 +651,16 @@ template <int EPI, int TN, int TM, int NT>
 __device__ __forceinline__ void ct_store(const GemmParams& p, const float* ct, int m0, int n0, int split) {
   constexpr int CLD = TN + 4;
   constexpr int CPR = TN / 8;  // 8-column chunks per row
+  if constexpr (EPI != EPI_SILU_MUL) {
+    store_pass<EPI, (TM * CPR + NT - 1) / NT, NT>(p, TM * CPR, split, [&](int c, int& m, int& n, const float*& src) {
+      const int row = c / CPR;
+      m = m0 + row;
+      n = n0 + (c % CPR) * 8;
+      src = ct + row * CLD + (c % CPR) * 8;
+      return m < p.M && n < p.N;
+    });
+    return;
+  }
   for (int c = threadIdx.x; c < TM * CPR; c += NT) {
     const int row = c / CPR, n = n0 + (c % CPR) * 8, m = m0 + row;
     if (m >= p.M || n >= p.N) continue;
@@ -683,8 +784,6 @@ constexpr int smem_ring() {
   return TM * (TN + 4) * 4 > SLOTS * (TM + TN) * TBK * 2 ? TM * (TN + 4) * 4 : SLOTS * (TM + TN) * TBK * 2;
 }
 
-// s_waitcnt immediate for vmcnt(n) alone (gfx9 layout: vmcnt[3:0] | vmcnt[5:4] << 14)
-constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
 
 // MI = 16-row MFMA tiles per wave: 4 (128-row tiles) or 3 (96-row tiles: a
 // 256-row decode GEMM as 3 row tiles -- 3/4 of the A bytes per workgroup
@@ -1189,7 +1288,10 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m
   float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // pass 0: every DMA landed before C overwrites the ring; pass 1: only the
+    // LDS reads of pass 0 (its stores stay in flight)
+    if (h == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if ((wc >> 1) == h) {
 #pragma unroll
@@ -1204,6 +1306,16 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(GemmParams p, int tiles_m
           }
     }
     __syncthreads();
+    if constexpr (EPI != EPI_SILU_MUL) {
+      store_pass<EPI, GBM * 16 / 512, 512>(p, GBM * 16, split, [&](int c, int& m, int& n, const float*& src) {
+        const int row = c >> 4, ch = c & 15;
+        m = m0 + row;
+        n = n0 + h * 128 + ch * 8;
+        src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+        return m < p.M && n < p.N;
+      });
+      continue;
+    }
     for (int c = threadIdx.x; c < GBM * 16; c += 512) {
       const int row = c >> 4, ch = c & 15, m = m0 + row, n = n0 + h * 128 + ch * 8;
       if (m >= p.M || n >= p.N) continue;
@@ -1457,7 +1569,10 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
   float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // pass 0: every DMA landed before C overwrites the ring; pass 1: only the
+    // LDS reads of pass 0 (its stores stay in flight)
+    if (h == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh)
@@ -1472,6 +1587,16 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
             ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[mh * 4 + i][h * 2 + j][q];
           }
     __syncthreads();
+    if constexpr (EPI != EPI_SILU_MUL) {
+      store_pass<EPI, 256 * 16 / 512, 512>(p, 256 * 16, split, [&](int c, int& m, int& n, const float*& src) {
+        const int row = c >> 4, ch = c & 15;
+        m = m0 + row;
+        n = n0 + h * 128 + ch * 8;
+        src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+        return m < p.M && n < p.N;
+      });
+      continue;
+    }
     for (int c = threadIdx.x; c < 256 * 16; c += 512) {
       const int row = c >> 4, ch = c & 15, m = m0 + row, n = n0 + h * 128 + ch * 8;
       if (m >= p.M || n >= p.N) continue;
@@ -1603,8 +1728,18 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
           }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      if constexpr (EPI != EPI_SILU_MUL) {
+        store_pass<EPI, 2, 512>(p, 64 * 16, 0, [&](int c, int& m, int& n, const float*& src) {
+          const int row = c >> 4, ch = c & 15;
+          m = m0 + mh * 128 + (row >> 5) * 64 + i2 * 32 + (row & 31);
+          n = n0 + nh * 128 + ch * 8;
+          src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+          return m < p.M && n < p.N;
+        });
+      }
 #pragma unroll
       for (int c0 = 0; c0 < 2; ++c0) {
+        if constexpr (EPI != EPI_SILU_MUL) break;
         const int c = (int)threadIdx.x + c0 * 512;
         const int row = c >> 4, ch = c & 15;
         const int m = m0 + mh * 128 + (row >> 5) * 64 + i2 * 32 + (row & 31);
@@ -1878,6 +2013,17 @@ __global__ __launch_bounds__(512) void gemm_d256_kernel(GemmParams p, int* __res
 #pragma unroll
       for (int q = 0; q < 4; ++q) ct[(w * 32 + i * 16 + 4 * g + q) * CLD + j * 16 + r] = acc[i][j][q];
   __syncthreads();
+  if constexpr (EPI != EPI_SILU_MUL) {
+    store_pass<EPI, (256 * CPR + 511) / 512, 512>(p, 256 * CPR, split, [&](int c, int& m, int& n, const float*& src) {
+      const int row = c / CPR, ch = c % CPR;
+      m = row;
+      n = n0 + ch * 8;
+      src = ct + row * CLD + ch * 8;
+      return m < p.M && n < p.N;
+    });
+    LSD_STAMP(3)
+    return;
+  }
   for (int c = threadIdx.x; c < 256 * CPR; c += 512) {
     const int row = c / CPR, ch = c % CPR, m = row, n = n0 + ch * 8;
     if (m >= p.M || n >= p.N) continue;

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __rest
                                                    const bf16* __restrict__ w,
                                                    const bf16* __restrict__ b, bf16* out, int T,
                                                    int H, float eps, const int* __restrict__ rows) {
-  __shared__ float red[16];
+  __shared__ float red[24];
   const int t = blockIdx.x;
   // gamma / beta are issued first: their latency overlaps the row loads
   // instead of adding a second memory round trip after the reductions
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __rest
   const int src = rows ? rows[t] : t;  // optional row gather (last-token rows)
   float* xr = x + (long)src * H;
   f32x4 v[MAXV];
-  float s1 = 0.f;
+  float s1 = 0.f, s2 = 0.f;
   // GRP column groups of the row are loaded per round trip (all of them
   // unless the slab count would blow the register budget)
   constexpr int NL = SPL > 0 ? SPL : 0;
@@ -106,24 +106,36 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __rest
         }
         v[i] = a;
         if (!RMS) s1 += a[0] + a[1] + a[2] + a[3];
+        else s2 += a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
       } else {
         v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
   }
   if (out == nullptr) return;  // combine-only (flush)
-  float mean = 0.f;
-  if (!RMS) mean = block_sum(s1, red) / H;
-  float s2 = 0.f;
+  // LayerNorm: each thread's (count, mean, M2) over its own <= 4 MAXV values
+  // (exact two-pass in registers), merged across the block in ONE LDS round
+  // (Chan) instead of a mean reduction followed by a variance reduction
+  float mean = 0.f, var;
+  if (RMS) {
+    var = block_sum(s2, red) / H;
+  } else {
+    float cnt = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = (threadIdx.x + i * 256) * 4;
-    if (c < H) {
-      f32x4 d = v[i] - mean;
-      s2 += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+    for (int i = 0; i < MAXV; ++i) cnt += (threadIdx.x + i * 256) * 4 < H ? 4.f : 0.f;
+    const float mt = cnt > 0.f ? s1 / cnt : 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      if ((threadIdx.x + i * 256) * 4 < H) {
+        const f32x4 d = v[i] - mt;
+        s2 += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+      }
     }
+    const Wf st = block_welford(Wf{cnt, mt, s2}, red);
+    mean = st.m;
+    var = st.M / H;
   }
-  const float rstd = rsqrtf(block_sum(s2, red) / H + eps);
+  const float rstd = rsqrtf(var + eps);
   bf16* o = out + (long)t * H;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
