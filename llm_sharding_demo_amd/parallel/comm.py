@@ -40,6 +40,8 @@ from typing import Dict, List, Optional
 
 import torch
 
+from ..utils import racecheck
+
 
 class TransportError(RuntimeError):
     pass
@@ -455,7 +457,7 @@ class GlooPlanChannel:
 # In-process fake transport (tests, single-process multi-stage)
 # ---------------------------------------------------------------------------
 
-class LocalFabric:
+class LocalFabric(racecheck.Shared):
     """Shared mailbox for P in-process stages.  fault: optional callable
     (edge, src, dst, seq) -> None | "drop" | float(delay seconds) | Exception."""
 
@@ -464,7 +466,7 @@ class LocalFabric:
         self.timeout = timeout
         self.fault = fault
         self._q: Dict[tuple, queue.Queue] = {}
-        self._lock = threading.Lock()
+        self._lock = racecheck.Lock("fabric")
         self._bcast: Dict[int, queue.Queue] = {r: queue.Queue() for r in range(num_stages)}
         self._seq: Dict[tuple, int] = {}
         self._barrier = threading.Barrier(num_stages)
@@ -488,12 +490,14 @@ class LocalFabric:
 
     def q(self, key) -> queue.Queue:
         with self._lock:
+            racecheck.note(self, "_q")
             if key not in self._q:
                 self._q[key] = queue.Queue()
             return self._q[key]
 
     def next_seq(self, key) -> int:
         with self._lock:
+            racecheck.note(self, "_seq")
             n = self._seq.get(key, 0)
             self._seq[key] = n + 1
             return n

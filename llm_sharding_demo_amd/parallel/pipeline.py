@@ -43,9 +43,10 @@ from ..models.stage import StageModel
 from ..runtime.batch import BatchMeta, SamplingState
 from ..runtime.plan import GroupPlan, StepPlan
 from ..utils.tracing import trace_range
+from ..utils import racecheck
 from .comm import Handle, SendHandle, Transport
 
-class _CaptureGate:
+class _CaptureGate(racecheck.Shared):
     """Stage threads sharing one GPU (local mode) issue work concurrently, but
     HIP rejects a stream capture that overlaps another thread's stream
     operations (hipErrorStreamCaptureIsolation) or a replay during a capture.
@@ -55,7 +56,7 @@ class _CaptureGate:
     process (dist, P = 1): always uncontended."""
 
     def __init__(self):
-        self._cv = threading.Condition()
+        self._cv = racecheck.Condition(name="capture_gate")
         self._readers = 0
         self._writer = False
         self._waiting = 0
@@ -128,7 +129,7 @@ class SamplingView:
         self.step.add_(self.active.to(self.step.dtype))
 
 
-class GroupState:
+class GroupState(racecheck.Shared):
     """Persistent per-(stage, group) device state: decode row metadata,
     sampler state, input / output buffers and the group's captured graphs."""
 
@@ -244,7 +245,7 @@ class StepStats:
                 "busy_fraction": round(busy / wall, 4) if wall > 0 else 0.0, "items": len(iv)}
 
 
-class StageWorker:
+class StageWorker(racecheck.Shared):
     def __init__(self, stage: StageModel, transport: Optional[Transport], stage_idx: int,
                  num_stages: int, scratch_slot: int = 0, compat_slot: int = 0,
                  wire: Optional[torch.dtype] = None):
@@ -357,6 +358,12 @@ class StageWorker:
         inside a session add no cross-stream hops: group g always runs on
         lanes[g % L], so its items are ordered by the lane itself (a per-step
         lane <-> stream event round trip costs ~0.2 ms of GPU idle)."""
+        # the calling (stage) thread owns this worker and its groups from here on:
+        # the hand-over from the constructing thread is ordered by the plan channel,
+        # which the lockset checker (utils/racecheck.py) cannot see
+        racecheck.handoff(self)
+        for gs in (getattr(self, "groups", None) or {}).values():
+            racecheck.handoff(gs)
         if not self.lanes:
             return
         with self._gpu():

@@ -32,11 +32,12 @@ import statistics
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
 from ..config import EngineConfig, SamplingParams
+from ..utils import racecheck
 from ..models.stage import StageModel
 from ..parallel.comm import (GlooPlanChannel, LocalFabric, LocalPlanChannel, Transport,
                              TransportError, init_distributed, make_dist_transport)
@@ -69,7 +70,7 @@ def resolve_device(spec: str) -> torch.device:
     return torch.device(spec)
 
 
-class Engine:
+class Engine(racecheck.Shared):
     def __init__(self, cfg: EngineConfig, mode: str = "local",
                  devices: Optional[Sequence[str]] = None, fault=None):
         self.cfg = cfg
@@ -104,8 +105,12 @@ class Engine:
         self._rng = random.Random(cfg.seed)
         self.healthy = True
         self.last_error: Optional[str] = None
-        self._lock = threading.RLock()
-        self.round_started: Optional[float] = None  # monotonic time of the last progress (watchdog)
+        self._lock = racecheck.RLock("engine")
+        # watchdog: per-thread monotonic start of the step each thread is inside (the
+        # serving driver and, in local mode, every stage follower); one shared slot
+        # let a follower's "done" clear the driver's in-flight start (found by
+        # utils/racecheck.py: two writers, no common lock)
+        self._rounds: Dict[int, Optional[float]] = {}
         self.max_seq = min(cfg.max_seq_len, self.mcfg.max_positions)
         self.last_session: Optional[SessionStats] = None
         self.loop_thread: Optional[threading.Thread] = None
@@ -191,6 +196,15 @@ class Engine:
             w.configure(self.M, self.group_cap)
 
     # ------------------------------------------------------------------
+    def _round(self, t: Optional[float]) -> None:
+        self._rounds[threading.get_ident()] = t  # each thread writes only its own key
+
+    @property
+    def round_started(self) -> Optional[float]:
+        """Start of the oldest step some thread is inside (None: none in flight)."""
+        starts = [v for v in list(self._rounds.values()) if v is not None]
+        return min(starts) if starts else None
+
     def _kv_slots(self, devices, collective: bool = False) -> int:
         """KV slots per stage: max_batch, capped by what fits the KV budget of
         free HBM (288 GB per MI355X) after the weights.  In
@@ -363,7 +377,8 @@ class Engine:
                 self._check_followers()
                 if not self.healthy:
                     raise RuntimeError(self.last_error)
-                self.round_started = t0 = time.monotonic()
+                t0 = time.monotonic()
+                self._round(t0)
                 nxt = sch.build_step()
                 self._send_plans(nxt)
                 t1 = time.monotonic()
@@ -400,7 +415,7 @@ class Engine:
             sch.fail_all(RuntimeError(f"engine unhealthy: {self.last_error}"))
             raise
         finally:
-            self.round_started = None
+            self._round(None)
         if timing and ran:
             self._finish_stats()
 
@@ -461,9 +476,9 @@ class Engine:
                 worker.start_stats()
                 started = True
             nxt = recv()
-            self.round_started = time.monotonic()  # watchdog: host blocked inside a step
+            self._round(time.monotonic())  # watchdog: host blocked inside a step
             worker.run_step(cur, nxt if not nxt.stop else None)
-            self.round_started = None
+            self._round(None)
             if not self.healthy:
                 raise RuntimeError(self.last_error)
             cur = nxt
@@ -472,9 +487,9 @@ class Engine:
         if not end_plan.timing:
             worker.stats = None
             return
-        self.round_started = time.monotonic()
+        self._round(time.monotonic())
         worker.sync()
-        self.round_started = None
+        self._round(None)
         st = worker.end_stats()
         if self.mode == "local":
             self._stats_q.put(st)

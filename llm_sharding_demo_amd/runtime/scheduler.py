@@ -40,6 +40,7 @@ from typing import Callable, Deque, Dict, List, Optional
 import torch
 
 from ..config import SamplingParams
+from ..utils import racecheck
 from .plan import Chunk, GroupPlan, Row, StepPlan
 
 log = logging.getLogger("llm_sharding_demo_amd.scheduler")
@@ -78,7 +79,7 @@ class Request:
         self._done.set()
 
 
-class PyBatchQueue:
+class PyBatchQueue(racecheck.Shared):
     """Pure-Python twin of the native `BatchQueue` (csrc/runtime/batch_queue.h):
     same interface and grouping rule; the reference the tests compare the
     native queue against, and the fallback when _runtime.so is absent."""
@@ -87,7 +88,7 @@ class PyBatchQueue:
         if max_batch < 1 or length_ratio < 1.0:
             raise ValueError("max_batch >= 1 and length_ratio >= 1 required")
         self.max_batch, self.ratio = max_batch, length_ratio
-        self._cv = threading.Condition()
+        self._cv = racecheck.Condition(name="batch_queue")
         self._q: "collections.deque" = collections.deque()
         self._closed = False
         self.max_seen = 0
@@ -461,7 +462,7 @@ class _Meta:
     done: bool = False  # finished by this scheduler (plain flag: the readout loop's hot path)
 
 
-class Scheduler:
+class Scheduler(racecheck.Shared):
     """Continuous-batching scheduler for one engine (every pipeline replica).
 
     Runs on the thread that drives stage 0 of replica 0 (`Engine._drive`);
@@ -476,13 +477,13 @@ class Scheduler:
         self.queue = make_batch_queue(max(1, cap * groups * self.R))
         self._pending: Dict[int, Request] = {}
         self._ids = itertools.count()
-        self._plock = threading.Lock()
+        self._plock = racecheck.Lock("sched.pending")
         self.meta: Dict[int, _Meta] = {}
         self.core = make_sched_core(self.R, groups, cap, engine.cfg.prefill_budget,
                                     engine.cfg.prefill_chunk, engine.max_seq, engine.slot_pools)
         self.step = 0
         self.readouts: Deque[tuple] = collections.deque()  # (step, ready(), sync(), tokens, key)
-        self.lock = threading.RLock()                       # one driver at a time
+        self.lock = racecheck.RLock("sched.driver")         # one driver at a time
         self.timing = False
         self.step_log: List[tuple] = []                     # (step, had_prefill) of timed steps
         self.stats = {"steps": 0, "joins": 0, "leaves": 0, "max_rows": 0, "captures": 0}
@@ -496,9 +497,11 @@ class Scheduler:
             return req
         rid = next(self._ids)
         with self._plock:
+            racecheck.note(self, "_pending")
             self._pending[rid] = req
         if not self.queue.push(rid, params.max_new_tokens):
             with self._plock:
+                racecheck.note(self, "_pending")
                 self._pending.pop(rid, None)
             raise RuntimeError("scheduler is closed")
         return req
@@ -510,6 +513,7 @@ class Scheduler:
     def _take_new(self) -> None:
         ids = self.queue.try_pop(1 << 20)
         with self._plock:
+            racecheck.note(self, "_pending")
             reqs = [(i, self._pending.pop(i)) for i in ids]
         for i, req in reqs:
             p = req.params
