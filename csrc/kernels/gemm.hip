@@ -1623,6 +1623,369 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
 }
 
 // ---------------------------------------------------------------------------
+// Prefill GEMM, one wave per SIMD (kind 7): 256x256 tile, 4 waves x 128x128
+// ---------------------------------------------------------------------------
+// hipBLASLt's bf16 kernel on these shapes is a 4-wave 256x256 design with 512
+// registers per wave (profiles/r3_pmc_p8_vs_hipblaslt.txt: SQ_WAVES = 4 per CU,
+// 74 % MFMA busy where the 8-wave p8 loop reaches 56 %).  Same idea here:
+//   * wave (wr, wc) owns a 128 x 128 output block: 64 16x16 accumulator tiles
+//     (256 registers, AGPRs), fragments for one 32-deep half k-step in 128
+//     more, double-buffered (R0 / R1);
+//   * each 64-deep k-tile is one LDS buffer (A 32 KiB | W 32 KiB, [256][64]
+//     lds_frag images), two buffers;
+//   * per k-tile: 64 MFMAs of half 0 beside the 16 fragment reads of half 1
+//     and half of the next k-tile's LDS-DMA (buffer_load ... lds), 48 MFMAs of
+//     half 1 beside the other half of the DMA, then vmcnt(0) + ONE barrier
+//     (the next buffer landed for every wave; every wave done reading the
+//     buffer refilled next), then the next k-tile's half-0 reads beside the
+//     last 16 MFMAs.  One wave per SIMD: a wave hides its own LDS / DMA issue
+//     between its MFMAs (sched_group_barrier interleave) instead of relying on
+//     a partner wave.
+constexpr int W4_OP = 256 * 64 * 2;    // 32 KiB per operand per k-tile
+constexpr int W4_BUF = 2 * W4_OP;      // A | W
+constexpr int W4_SMEM = 2 * W4_BUF;    // 128 KiB (== 256 x 128 fp32 C half-tile)
+
+template <int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm_w4_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
+  __shared__ __attribute__((aligned(16))) char smem[W4_SMEM];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  tile_order(bid, tiles_m, tiles_n, G, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int T = p.K / 64;
+  const int lane = lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int r = lane & 15, g = lane >> 4;
+
+  // this wave's 8 LDS-DMA instructions (64 rows x 128 B) of one operand of k-tile kt
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)m0 * p.lda), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (long)n0 * p.ldw), 0, 0x7fffffff, 0x00020000);
+  int offa[8], offw[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int row = (w * 8 + q) * 8 + (lane >> 3);
+    const int lch = (lane & 7) ^ ((row >> 1) & 7);
+    offa[q] = ((min(m0 + row, p.M - 1) - m0) * p.lda + lch * 8) * 2;
+    offw[q] = ((min(n0 + row, p.N - 1) - n0) * p.ldw + lch * 8) * 2;
+  }
+  // instructions [q0, q0 + nq) of A then W of k-tile kt into buffer `b` (branch-free
+  // loop body: the last iteration re-stages its own k-tile into the idle buffer)
+  auto dma = [&](int kt, int b, int q0, int nq) {
+    char* buf = smem + b * W4_BUF;
+    const int kb = kt * 128;  // byte offset of the k-tile in a row
+#pragma unroll
+    for (int q = q0; q < q0 + nq; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(buf + (w * 8 + q) * 1024), 16, offa[q], kb, 0, 0);
+#pragma unroll
+    for (int q = q0; q < q0 + nq; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(buf + W4_OP + (w * 8 + q) * 1024), 16, offw[q], kb,
+                                                0, 0);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  auto frags = [&](int kt, int kk, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
+    const char* buf = smem + (kt & 1) * W4_BUF;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = lds_frag(buf, wr * 128 + i * 16 + r, kk * 4 + g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bf[j] = lds_frag(buf + W4_OP, wc * 128 + j * 16 + r, kk * 4 + g);
+  };
+  // MFMAs of tiles [t0, t1) of the 8 x 8 block (row-major), with operands (af, bf)
+  auto mma = [&](bf16x8 (&af)[8], bf16x8 (&bf)[8], int t0, int t1) {
+#pragma unroll
+    for (int t = t0; t < t1; ++t) acc[t >> 3][t & 7] = mfma16(af[t >> 3], bf[t & 7], acc[t >> 3][t & 7]);
+  };
+
+  if (T > 0) {
+    dma(0, 0, 0, 8);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    frags(0, 0, a0, b0);
+    for (int t = 0; t < T; ++t) {
+      const int kn = t + 1 < T ? t + 1 : t, bn = (t + 1) & 1;
+      // half 0: 64 MFMAs | half-1 fragment reads (16) | DMA of t+1, A / W instructions 0-3 (8)
+      dma(kn, bn, 0, 4);
+      frags(t, 1, a1, b1);
+      mma(a0, b0, 0, 64);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
+      }
+      // half 1: 48 MFMAs | DMA of t+1, instructions 4-7
+      dma(kn, bn, 4, 4);
+      mma(a1, b1, 0, 48);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 1);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // k-tile t+1 landed for every wave; every wave done reading buffer t (its
+      // half-1 reads completed before its MFMAs above)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      frags(t + 1, 0, a0, b0);  // buffer (t+1) & 1 (a re-staged copy of k-tile t on the last one)
+      mma(a1, b1, 48, 64);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // Epilogue: two passes over 128-column halves (the waves with wc == h write
+  // their 128 x 128 block), C staged as fp32 [256][128] in LDS (16-float chunks
+  // XOR-swizzled by (row >> 2) & 3), then row-contiguous 16-byte stores.
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wc == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = wr * 128 + i * 16 + 4 * g + q;
+            const int col = j * 16 + r;
+            ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][q];
+          }
+    }
+    __syncthreads();
+    if constexpr (EPI != EPI_SILU_MUL) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)  // 8 chunks per thread per store pass (register budget)
+        store_pass<EPI, 8, 256>(p, 128 * 16, 0, [&](int c, int& m, int& n, const float*& src) {
+          const int row = sub * 128 + (c >> 4), ch = c & 15;
+          m = m0 + row;
+          n = n0 + h * 128 + ch * 8;
+          src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+          return m < p.M && n < p.N;
+        });
+      continue;
+    }
+    for (int c = threadIdx.x; c < 256 * 16; c += 256) {
+      const int row = c >> 4, ch = c & 15, m = m0 + row, n = n0 + h * 128 + ch * 8;
+      if (m >= p.M || n >= p.N || (ch & 3) >= 2) continue;  // up chunks are read by their gate chunk
+      const float* src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+      const float* up = ct + row * 128 + (((ch + 2) * 8) ^ (((row >> 2) & 3) << 4));
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src), hi = *reinterpret_cast<const f32x4*>(src + 4);
+      const f32x4 ulo = *reinterpret_cast<const f32x4*>(up), uhi = *reinterpret_cast<const f32x4*>(up + 4);
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
+      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
+    }
+  }
+}
+
+// Kind 8: the same one-wave-per-SIMD schedule on v_mfma_f32_32x32x16_bf16: half
+// the MFMA instructions (32 cycles each), so twice the issue slots per MFMA gap
+// for the interleaved fragment reads and LDS-DMA.  A / B fragments of a 16-deep
+// k-step are one ds_read_b128 per lane of the same [256][64] image (lane l: row
+// l & 31, 16-byte chunk 2 ks + (l >> 5): conflict-free under the lds_frag swizzle).
+// SCH 1 (kind 9): all 16 LDS-DMA instructions of k-tile t+1 beside half 0, the barrier after
+// 16 of half 1's 32 MFMAs, so the next k-tile's half-0 fragment reads hide under the last 16.
+template <int EPI, int SCH = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm_w5_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
+  __shared__ __attribute__((aligned(16))) char smem[W4_SMEM];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int tm, tn;
+  tile_order(bid, tiles_m, tiles_n, G, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int T = p.K / 64;
+  const int lane = lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int r32 = lane & 31, h32 = lane >> 5;
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)m0 * p.lda), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (long)n0 * p.ldw), 0, 0x7fffffff, 0x00020000);
+  int offa[8], offw[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int row = (w * 8 + q) * 8 + (lane >> 3);
+    const int lch = (lane & 7) ^ ((row >> 1) & 7);
+    offa[q] = ((min(m0 + row, p.M - 1) - m0) * p.lda + lch * 8) * 2;
+    offw[q] = ((min(n0 + row, p.N - 1) - n0) * p.ldw + lch * 8) * 2;
+  }
+  auto dma = [&](int kt, int b, int q0, int nq) {
+    char* buf = smem + b * W4_BUF;
+    const int kb = kt * 128;
+#pragma unroll
+    for (int q = q0; q < q0 + nq; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(buf + (w * 8 + q) * 1024), 16, offa[q], kb, 0, 0);
+#pragma unroll
+    for (int q = q0; q < q0 + nq; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(buf + W4_OP + (w * 8 + q) * 1024), 16, offw[q], kb,
+                                                0, 0);
+  };
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // half hh of k-tile kt: 16-deep k-steps 2 hh, 2 hh + 1; [s][i] = k-step s, 32-row block i
+  bf16x8 a0[2][4], b0[2][4], a1[2][4], b1[2][4];
+  auto frags = [&](int kt, int hh, bf16x8 (&af)[2][4], bf16x8 (&bf)[2][4]) {
+    const char* buf = smem + (kt & 1) * W4_BUF;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int ch = 2 * (2 * hh + s2) + h32;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[s2][i] = lds_frag(buf, wr * 128 + i * 32 + r32, ch);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[s2][j] = lds_frag(buf + W4_OP, wc * 128 + j * 32 + r32, ch);
+    }
+  };
+  auto mma = [&](bf16x8 (&af)[2][4], bf16x8 (&bf)[2][4], int t0, int t1) {  // t = s2 * 16 + i * 4 + j
+#pragma unroll
+    for (int t = t0; t < t1; ++t) {
+      const int s2 = t >> 4, i = (t >> 2) & 3, j = t & 3;
+      acc[i][j] = mfma32(af[s2][i], bf[s2][j], acc[i][j]);
+    }
+  };
+
+  if (T > 0) {
+    dma(0, 0, 0, 8);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    frags(0, 0, a0, b0);
+    for (int t = 0; t < T; ++t) {
+      const int kn = t + 1 < T ? t + 1 : t, bn = (t + 1) & 1;
+      if constexpr (SCH == 1) {
+        dma(kn, bn, 0, 8);
+        frags(t, 1, a1, b1);
+        mma(a0, b0, 0, 32);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+        mma(a1, b1, 0, 16);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        frags(t + 1, 0, a0, b0);
+        mma(a1, b1, 16, 32);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
+      dma(kn, bn, 0, 4);
+      frags(t, 1, a1, b1);
+      mma(a0, b0, 0, 32);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
+      }
+      dma(kn, bn, 4, 4);
+      mma(a1, b1, 0, 24);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      frags(t + 1, 0, a0, b0);
+      mma(a1, b1, 24, 32);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wc == h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h32;
+            const int col = j * 32 + r32;
+            ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][e];
+          }
+    }
+    __syncthreads();
+    if constexpr (EPI != EPI_SILU_MUL) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+        store_pass<EPI, 8, 256>(p, 128 * 16, 0, [&](int c, int& m, int& n, const float*& src) {
+          const int row = sub * 128 + (c >> 4), ch = c & 15;
+          m = m0 + row;
+          n = n0 + h * 128 + ch * 8;
+          src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+          return m < p.M && n < p.N;
+        });
+      continue;
+    }
+    for (int c = threadIdx.x; c < 256 * 16; c += 256) {
+      const int row = c >> 4, ch = c & 15, m = m0 + row, n = n0 + h * 128 + ch * 8;
+      if (m >= p.M || n >= p.N || (ch & 3) >= 2) continue;
+      const float* src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
+      const float* up = ct + row * 128 + (((ch + 2) * 8) ^ (((row >> 2) & 3) << 4));
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src), hi = *reinterpret_cast<const f32x4*>(src + 4);
+      const f32x4 ulo = *reinterpret_cast<const f32x4*>(up), uhi = *reinterpret_cast<const f32x4*>(up + 4);
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
+      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Persistent prefill GEMM (kind 6): the p8 k-loop as one stream across tiles
 // ---------------------------------------------------------------------------
 // gridDim.x (a multiple of 8, <= the CU count) workgroups; workgroup b runs the
@@ -2202,6 +2565,12 @@ static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStre
     else if (g_big_kind == 5)
       hipLaunchKernelGGL((gemm_p8_kernel<EPI, 5>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
                          g_big_group);
+    else if (g_big_kind == 9 && p.splits == 1)
+      hipLaunchKernelGGL((gemm_w5_kernel<EPI, 1>), dim3(bm * bn), dim3(256), 0, st, p, bm, bn, g_big_group);
+    else if (g_big_kind == 8 && p.splits == 1)
+      hipLaunchKernelGGL((gemm_w5_kernel<EPI>), dim3(bm * bn), dim3(256), 0, st, p, bm, bn, g_big_group);
+    else if (g_big_kind == 7 && p.splits == 1)
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI>), dim3(bm * bn), dim3(256), 0, st, p, bm, bn, g_big_group);
     else if (g_big_kind == 6 && p.splits == 1 && p.K >= 128 && bm * bn >= pp_grid())
       hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(pp_grid()), dim3(512), 0, st, p, bm, bn, g_big_group);
     else if (g_big_kind == 6)
@@ -2285,7 +2654,7 @@ using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
 extern "C" void lsd_gemm_set_big_group(int v) { g_big_group = v < 0 ? 0 : v; }
-extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v >= 0 && v <= 6) ? v : 0; }
+extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v >= 0 && v <= 9) ? v : 0; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }
