@@ -25,6 +25,8 @@
 // store, residual add into the fp32 residual stream, split-K slab, and the
 // QKV epilogue that applies RoPE (Llama) and scatters K/V straight into the
 // shard-local KV cache at (slot, position).
+#include <type_traits>
+
 #include "common.h"
 #include "gemm_params.h"
 
@@ -1404,7 +1406,8 @@ __device__ __forceinline__ void p8_stage(char* lds, const bf16* src, long ld, in
 // VAR (A/B, gemm_set_big_kind 2/3): bit 0 issues each phase's LDS-DMA before its
 // fragment reads (p8 loop stamps: a glds issued behind 12 ds_read_b128 costs the wave
 // 100+ cycles); bit 1 reads q0's B fragments before its A fragments; bit 2 stages
-// with buffer_load ... lds (32-bit lane offsets) instead of global_load_lds.
+// with buffer_load ... lds (32-bit lane offsets) instead of global_load_lds; bit 3
+// peels the k-loop (steady-state body without the t+1 / t+2 branches).
 template <int EPI, int VAR = 0>
 __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
   __shared__ __attribute__((aligned(16))) char smem[P8_SMEM];
@@ -1498,8 +1501,10 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
 #ifdef LSD_P8_PROF
     pf_t0 = P8_T();
 #endif
-    for (int t = 0; t < T; ++t) {
-      const bool n1 = t + 1 < T, n2 = t + 2 < T;
+    // one k-tile; n1 / n2 (k-tiles t+1 / t+2 exist) are bools, or std::integral_constant
+    // in the peeled form (VAR bit 3), where the branches fold away
+    auto body = [&](int t, auto N1, auto N2) {
+      const bool n1 = static_cast<bool>(N1), n2 = static_cast<bool>(N2);
       // q0: (A0, B0)
       if constexpr ((VAR & 1) != 0) {
         if (n1) stage(t + 1, 3);
@@ -1548,6 +1553,14 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
                     else if (n1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"))
       __builtin_amdgcn_sched_barrier(0);
       mma(1, 0, b0);
+    };
+    if constexpr ((VAR & 8) != 0) {  // peeled: steady state without per-phase branches
+      int t = 0;
+      for (; t + 2 < T; ++t) body(t, std::true_type{}, std::true_type{});
+      if (t + 1 < T) body(t++, std::true_type{}, std::false_type{});
+      body(t, std::false_type{}, std::false_type{});
+    } else {
+      for (int t = 0; t < T; ++t) body(t, t + 1 < T, t + 2 < T);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 #ifdef LSD_P8_PROF
@@ -2565,6 +2578,9 @@ static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStre
     else if (g_big_kind == 5)
       hipLaunchKernelGGL((gemm_p8_kernel<EPI, 5>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
                          g_big_group);
+    else if (g_big_kind == 10)
+      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 12>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+                         g_big_group);
     else if (g_big_kind == 9 && p.splits == 1)
       hipLaunchKernelGGL((gemm_w5_kernel<EPI, 1>), dim3(bm * bn), dim3(256), 0, st, p, bm, bn, g_big_group);
     else if (g_big_kind == 8 && p.splits == 1)
@@ -2654,7 +2670,7 @@ using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
 extern "C" void lsd_gemm_set_big_group(int v) { g_big_group = v < 0 ? 0 : v; }
-extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v >= 0 && v <= 9) ? v : 0; }
+extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v >= 0 && v <= 10) ? v : 0; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }

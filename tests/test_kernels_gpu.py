@@ -337,11 +337,12 @@ def BIG(C):
     C.gemm_set_big_min(160)
 
 
-@pytest.fixture(params=[4, 1, 0, 7, 8, 9])
+@pytest.fixture(params=[4, 1, 0, 7, 8, 9, 10])
 def BIGK(BIG, request):
     """The 256x256 kernel kinds: 4 = phase-pipelined BK=64 with buffer_load ... lds staging
     (default), 1 = the same with global_load_lds, 0 = the BK=32 4-slot ring, 7 = one wave per SIMD
-    (4 waves x 128x128), 8 = 7 on 32x32x16 MFMAs, 9 = 8 with the DMA beside half 0."""
+    (4 waves x 128x128), 8 = 7 on 32x32x16 MFMAs, 9 = 8 with the DMA beside half 0, 10 = 4 with
+    the k-loop peeled."""
     BIG.gemm_set_big_kind(request.param)
     yield BIG
     BIG.gemm_set_big_kind(4)
