@@ -25,8 +25,6 @@
 // store, residual add into the fp32 residual stream, split-K slab, and the
 // QKV epilogue that applies RoPE (Llama) and scatters K/V straight into the
 // shard-local KV cache at (slot, position).
-#include <type_traits>
-
 #include "common.h"
 #include "gemm_params.h"
 
@@ -1403,11 +1401,11 @@ __device__ __forceinline__ void p8_stage(char* lds, const bf16* src, long ld, in
   }
 }
 
-// VAR (A/B, gemm_set_big_kind 2/3): bit 0 issues each phase's LDS-DMA before its
-// fragment reads (p8 loop stamps: a glds issued behind 12 ds_read_b128 costs the wave
-// 100+ cycles); bit 1 reads q0's B fragments before its A fragments; bit 2 stages
-// with buffer_load ... lds (32-bit lane offsets) instead of global_load_lds; bit 3
-// peels the k-loop (steady-state body without the t+1 / t+2 branches).
+// VAR 4 (default, gemm_set_big_kind 4): stage with buffer_load ... lds (wave-uniform
+// resource, 32-bit lane offsets) instead of global_load_lds with 64-bit lane addresses;
+// VAR 0 = kind 1.  Issuing each phase's DMA before its fragment reads, B fragments first
+// and a peeled k-loop were measured and removed (profiles/r3_p8_buffer_lds.log,
+// r3_rejected_p8_peeled_loop.log).
 template <int EPI, int VAR = 0>
 __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
   __shared__ __attribute__((aligned(16))) char smem[P8_SMEM];
@@ -1501,50 +1499,24 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
 #ifdef LSD_P8_PROF
     pf_t0 = P8_T();
 #endif
-    // one k-tile; n1 / n2 (k-tiles t+1 / t+2 exist) are bools, or std::integral_constant
-    // in the peeled form (VAR bit 3), where the branches fold away
-    auto body = [&](int t, auto N1, auto N2) {
-      const bool n1 = static_cast<bool>(N1), n2 = static_cast<bool>(N2);
+    for (int t = 0; t < T; ++t) {
+      const bool n1 = t + 1 < T, n2 = t + 2 < T;
       // q0: (A0, B0)
-      if constexpr ((VAR & 1) != 0) {
-        if (n1) stage(t + 1, 3);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr ((VAR & 2) != 0) {
-        read_b(t, 0, b0);
-        __builtin_amdgcn_sched_barrier(0);
-        read_a(t, 0);
-      } else {
-        read_a(t, 0);
-        read_b(t, 0, b0);
-      }
-      if constexpr ((VAR & 1) == 0) {
-        if (n1) stage(t + 1, 3);
-      }
+      read_a(t, 0);
+      read_b(t, 0, b0);
+      if (n1) stage(t + 1, 3);
       __builtin_amdgcn_sched_barrier(0);
       mma(0, 0, b0);
       // q1: (A0, B1); retire A1(t): 4 later halves in flight when t + 1 exists
-      if constexpr ((VAR & 1) != 0) {
-        if (n1) stage(t + 1, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        read_b(t, 1, b1);
-      } else {
-        read_b(t, 1, b1);
-        if (n1) stage(t + 1, 1);
-      }
+      read_b(t, 1, b1);
+      if (n1) stage(t + 1, 1);
       P8_ACC(pf_vm, if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
                     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory"))
       __builtin_amdgcn_sched_barrier(0);
       mma(0, 1, b1);
       // q2: (A1, B1)
-      if constexpr ((VAR & 1) != 0) {
-        if (n2) stage(t + 2, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        read_a(t, 1);
-      } else {
-        read_a(t, 1);
-        if (n2) stage(t + 2, 0);
-      }
+      read_a(t, 1);
+      if (n2) stage(t + 2, 0);
       __builtin_amdgcn_sched_barrier(0);
       mma(1, 1, b1);
       // q3: (A1, B0); retire A0 / B0 / B1 of t + 1 (A1(t+1), A0 / B0(t+2) stay in flight)
@@ -1553,14 +1525,6 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
                     else if (n1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"))
       __builtin_amdgcn_sched_barrier(0);
       mma(1, 0, b0);
-    };
-    if constexpr ((VAR & 8) != 0) {  // peeled: steady state without per-phase branches
-      int t = 0;
-      for (; t + 2 < T; ++t) body(t, std::true_type{}, std::true_type{});
-      if (t + 1 < T) body(t++, std::true_type{}, std::false_type{});
-      body(t, std::false_type{}, std::false_type{});
-    } else {
-      for (int t = 0; t < T; ++t) body(t, t + 1 < T, t + 2 < T);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 #ifdef LSD_P8_PROF
@@ -1635,582 +1599,11 @@ __global__ __launch_bounds__(512) void gemm_p8_kernel(GemmParams p, int tiles_m,
   LSD_STAMP(3)
 }
 
-// ---------------------------------------------------------------------------
-// Prefill GEMM, one wave per SIMD (kind 7): 256x256 tile, 4 waves x 128x128
-// ---------------------------------------------------------------------------
-// hipBLASLt's bf16 kernel on these shapes is a 4-wave 256x256 design with 512
-// registers per wave (profiles/r3_pmc_p8_vs_hipblaslt.txt: SQ_WAVES = 4 per CU,
-// 74 % MFMA busy where the 8-wave p8 loop reaches 56 %).  Same idea here:
-//   * wave (wr, wc) owns a 128 x 128 output block: 64 16x16 accumulator tiles
-//     (256 registers, AGPRs), fragments for one 32-deep half k-step in 128
-//     more, double-buffered (R0 / R1);
-//   * each 64-deep k-tile is one LDS buffer (A 32 KiB | W 32 KiB, [256][64]
-//     lds_frag images), two buffers;
-//   * per k-tile: 64 MFMAs of half 0 beside the 16 fragment reads of half 1
-//     and half of the next k-tile's LDS-DMA (buffer_load ... lds), 48 MFMAs of
-//     half 1 beside the other half of the DMA, then vmcnt(0) + ONE barrier
-//     (the next buffer landed for every wave; every wave done reading the
-//     buffer refilled next), then the next k-tile's half-0 reads beside the
-//     last 16 MFMAs.  One wave per SIMD: a wave hides its own LDS / DMA issue
-//     between its MFMAs (sched_group_barrier interleave) instead of relying on
-//     a partner wave.
-constexpr int W4_OP = 256 * 64 * 2;    // 32 KiB per operand per k-tile
-constexpr int W4_BUF = 2 * W4_OP;      // A | W
-constexpr int W4_SMEM = 2 * W4_BUF;    // 128 KiB (== 256 x 128 fp32 C half-tile)
-
-template <int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void gemm_w4_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
-  __shared__ __attribute__((aligned(16))) char smem[W4_SMEM];
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  int tm, tn;
-  tile_order(bid, tiles_m, tiles_n, G, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int T = p.K / 64;
-  const int lane = lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int r = lane & 15, g = lane >> 4;
-
-  // this wave's 8 LDS-DMA instructions (64 rows x 128 B) of one operand of k-tile kt
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)m0 * p.lda), 0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (long)n0 * p.ldw), 0, 0x7fffffff, 0x00020000);
-  int offa[8], offw[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int row = (w * 8 + q) * 8 + (lane >> 3);
-    const int lch = (lane & 7) ^ ((row >> 1) & 7);
-    offa[q] = ((min(m0 + row, p.M - 1) - m0) * p.lda + lch * 8) * 2;
-    offw[q] = ((min(n0 + row, p.N - 1) - n0) * p.ldw + lch * 8) * 2;
-  }
-  // instructions [q0, q0 + nq) of A then W of k-tile kt into buffer `b` (branch-free
-  // loop body: the last iteration re-stages its own k-tile into the idle buffer)
-  auto dma = [&](int kt, int b, int q0, int nq) {
-    char* buf = smem + b * W4_BUF;
-    const int kb = kt * 128;  // byte offset of the k-tile in a row
-#pragma unroll
-    for (int q = q0; q < q0 + nq; ++q)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(buf + (w * 8 + q) * 1024), 16, offa[q], kb, 0, 0);
-#pragma unroll
-    for (int q = q0; q < q0 + nq; ++q)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(buf + W4_OP + (w * 8 + q) * 1024), 16, offw[q], kb,
-                                                0, 0);
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
-  auto frags = [&](int kt, int kk, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
-    const char* buf = smem + (kt & 1) * W4_BUF;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = lds_frag(buf, wr * 128 + i * 16 + r, kk * 4 + g);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bf[j] = lds_frag(buf + W4_OP, wc * 128 + j * 16 + r, kk * 4 + g);
-  };
-  // MFMAs of tiles [t0, t1) of the 8 x 8 block (row-major), with operands (af, bf)
-  auto mma = [&](bf16x8 (&af)[8], bf16x8 (&bf)[8], int t0, int t1) {
-#pragma unroll
-    for (int t = t0; t < t1; ++t) acc[t >> 3][t & 7] = mfma16(af[t >> 3], bf[t & 7], acc[t >> 3][t & 7]);
-  };
-
-  if (T > 0) {
-    dma(0, 0, 0, 8);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    frags(0, 0, a0, b0);
-    for (int t = 0; t < T; ++t) {
-      const int kn = t + 1 < T ? t + 1 : t, bn = (t + 1) & 1;
-      // half 0: 64 MFMAs | half-1 fragment reads (16) | DMA of t+1, A / W instructions 0-3 (8)
-      dma(kn, bn, 0, 4);
-      frags(t, 1, a1, b1);
-      mma(a0, b0, 0, 64);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
-      }
-      // half 1: 48 MFMAs | DMA of t+1, instructions 4-7
-      dma(kn, bn, 4, 4);
-      mma(a1, b1, 0, 48);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 6, 1);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // k-tile t+1 landed for every wave; every wave done reading buffer t (its
-      // half-1 reads completed before its MFMAs above)
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      frags(t + 1, 0, a0, b0);  // buffer (t+1) & 1 (a re-staged copy of k-tile t on the last one)
-      mma(a1, b1, 48, 64);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 2);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-
-  // Epilogue: two passes over 128-column halves (the waves with wc == h write
-  // their 128 x 128 block), C staged as fp32 [256][128] in LDS (16-float chunks
-  // XOR-swizzled by (row >> 2) & 3), then row-contiguous 16-byte stores.
-  float* ct = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (h == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (wc == h) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int row = wr * 128 + i * 16 + 4 * g + q;
-            const int col = j * 16 + r;
-            ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][q];
-          }
-    }
-    __syncthreads();
-    if constexpr (EPI != EPI_SILU_MUL) {
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub)  // 8 chunks per thread per store pass (register budget)
-        store_pass<EPI, 8, 256>(p, 128 * 16, 0, [&](int c, int& m, int& n, const float*& src) {
-          const int row = sub * 128 + (c >> 4), ch = c & 15;
-          m = m0 + row;
-          n = n0 + h * 128 + ch * 8;
-          src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
-          return m < p.M && n < p.N;
-        });
-      continue;
-    }
-    for (int c = threadIdx.x; c < 256 * 16; c += 256) {
-      const int row = c >> 4, ch = c & 15, m = m0 + row, n = n0 + h * 128 + ch * 8;
-      if (m >= p.M || n >= p.N || (ch & 3) >= 2) continue;  // up chunks are read by their gate chunk
-      const float* src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
-      const float* up = ct + row * 128 + (((ch + 2) * 8) ^ (((row >> 2) & 3) << 4));
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(src), hi = *reinterpret_cast<const f32x4*>(src + 4);
-      const f32x4 ulo = *reinterpret_cast<const f32x4*>(up), uhi = *reinterpret_cast<const f32x4*>(up + 4);
-      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
-      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
-    }
-  }
-}
-
-// Kind 8: the same one-wave-per-SIMD schedule on v_mfma_f32_32x32x16_bf16: half
-// the MFMA instructions (32 cycles each), so twice the issue slots per MFMA gap
-// for the interleaved fragment reads and LDS-DMA.  A / B fragments of a 16-deep
-// k-step are one ds_read_b128 per lane of the same [256][64] image (lane l: row
-// l & 31, 16-byte chunk 2 ks + (l >> 5): conflict-free under the lds_frag swizzle).
-// SCH 1 (kind 9): all 16 LDS-DMA instructions of k-tile t+1 beside half 0, the barrier after
-// 16 of half 1's 32 MFMAs, so the next k-tile's half-0 fragment reads hide under the last 16.
-template <int EPI, int SCH = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void gemm_w5_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
-  __shared__ __attribute__((aligned(16))) char smem[W4_SMEM];
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  int tm, tn;
-  tile_order(bid, tiles_m, tiles_n, G, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int T = p.K / 64;
-  const int lane = lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int r32 = lane & 31, h32 = lane >> 5;
-
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)m0 * p.lda), 0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (long)n0 * p.ldw), 0, 0x7fffffff, 0x00020000);
-  int offa[8], offw[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int row = (w * 8 + q) * 8 + (lane >> 3);
-    const int lch = (lane & 7) ^ ((row >> 1) & 7);
-    offa[q] = ((min(m0 + row, p.M - 1) - m0) * p.lda + lch * 8) * 2;
-    offw[q] = ((min(n0 + row, p.N - 1) - n0) * p.ldw + lch * 8) * 2;
-  }
-  auto dma = [&](int kt, int b, int q0, int nq) {
-    char* buf = smem + b * W4_BUF;
-    const int kb = kt * 128;
-#pragma unroll
-    for (int q = q0; q < q0 + nq; ++q)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(buf + (w * 8 + q) * 1024), 16, offa[q], kb, 0, 0);
-#pragma unroll
-    for (int q = q0; q < q0 + nq; ++q)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void*)(buf + W4_OP + (w * 8 + q) * 1024), 16, offw[q], kb,
-                                                0, 0);
-  };
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  // half hh of k-tile kt: 16-deep k-steps 2 hh, 2 hh + 1; [s][i] = k-step s, 32-row block i
-  bf16x8 a0[2][4], b0[2][4], a1[2][4], b1[2][4];
-  auto frags = [&](int kt, int hh, bf16x8 (&af)[2][4], bf16x8 (&bf)[2][4]) {
-    const char* buf = smem + (kt & 1) * W4_BUF;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int ch = 2 * (2 * hh + s2) + h32;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[s2][i] = lds_frag(buf, wr * 128 + i * 32 + r32, ch);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[s2][j] = lds_frag(buf + W4_OP, wc * 128 + j * 32 + r32, ch);
-    }
-  };
-  auto mma = [&](bf16x8 (&af)[2][4], bf16x8 (&bf)[2][4], int t0, int t1) {  // t = s2 * 16 + i * 4 + j
-#pragma unroll
-    for (int t = t0; t < t1; ++t) {
-      const int s2 = t >> 4, i = (t >> 2) & 3, j = t & 3;
-      acc[i][j] = mfma32(af[s2][i], bf[s2][j], acc[i][j]);
-    }
-  };
-
-  if (T > 0) {
-    dma(0, 0, 0, 8);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    frags(0, 0, a0, b0);
-    for (int t = 0; t < T; ++t) {
-      const int kn = t + 1 < T ? t + 1 : t, bn = (t + 1) & 1;
-      if constexpr (SCH == 1) {
-        dma(kn, bn, 0, 8);
-        frags(t, 1, a1, b1);
-        mma(a0, b0, 0, 32);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-        }
-        mma(a1, b1, 0, 16);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        frags(t + 1, 0, a0, b0);
-        mma(a1, b1, 16, 32);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        continue;
-      }
-      dma(kn, bn, 0, 4);
-      frags(t, 1, a1, b1);
-      mma(a0, b0, 0, 32);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
-      }
-      dma(kn, bn, 4, 4);
-      mma(a1, b1, 0, 24);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 3, 1);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      frags(t + 1, 0, a0, b0);
-      mma(a1, b1, 24, 32);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-
-  float* ct = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (h == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (wc == h) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int row = wr * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h32;
-            const int col = j * 32 + r32;
-            ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[i][j][e];
-          }
-    }
-    __syncthreads();
-    if constexpr (EPI != EPI_SILU_MUL) {
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
-        store_pass<EPI, 8, 256>(p, 128 * 16, 0, [&](int c, int& m, int& n, const float*& src) {
-          const int row = sub * 128 + (c >> 4), ch = c & 15;
-          m = m0 + row;
-          n = n0 + h * 128 + ch * 8;
-          src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
-          return m < p.M && n < p.N;
-        });
-      continue;
-    }
-    for (int c = threadIdx.x; c < 256 * 16; c += 256) {
-      const int row = c >> 4, ch = c & 15, m = m0 + row, n = n0 + h * 128 + ch * 8;
-      if (m >= p.M || n >= p.N || (ch & 3) >= 2) continue;
-      const float* src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
-      const float* up = ct + row * 128 + (((ch + 2) * 8) ^ (((row >> 2) & 3) << 4));
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(src), hi = *reinterpret_cast<const f32x4*>(src + 4);
-      const f32x4 ulo = *reinterpret_cast<const f32x4*>(up), uhi = *reinterpret_cast<const f32x4*>(up + 4);
-      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const float u[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(v[e]) * u[e]);
-      st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent prefill GEMM (kind 6): the p8 k-loop as one stream across tiles
-// ---------------------------------------------------------------------------
-// gridDim.x (a multiple of 8, <= the CU count) workgroups; workgroup b runs the
-// tiles b, b + gridDim.x, ... in the launch-per-tile kernel's XCD-aware order
-// (xcd_remap of the virtual block id keeps every tile on the XCD it had there).
-// Its tiles' 64-deep k-tiles form ONE stream u = 0 .. ntiles * T - 1 and the p8
-// half-tile DMA schedule (q0 B1(u+1), q1 A1(u+1), q2 A0(u+2), q3 B0(u+2)) runs on
-// across tile boundaries, so the next tile's first k-tile and a half are in
-// flight while a tile's epilogue runs, and no workgroup pays a launch, a
-// prologue or a cold pipeline per tile (p8 stamps: prologue 1.7 us + epilogue
-// 8-12 us of a 62 us K = 1600 block, profiles/r2_p8_stamps_lmhead.log).
-// The epilogue stages C through 32 KiB of LDS of its own (8 passes of 64 rows
-// x 128 columns: every wave contributes a 32 x 32 block per pass), outside the
-// 128 KiB operand ring, with raw s_barriers behind lgkmcnt(0) waits only: the
-// operand DMA in flight is never drained by it.  Its global loads / stores are
-// younger than every staged half-tile, so the counted vmcnt waits of the next
-// k-tiles still retire what they retired (they may wait longer, never less).
-// The wave-row stagger is undone before an epilogue and redone after it.
-// splits == 1 only (one k-range per tile).  A/B only (gemm_set_big_kind(6)): measured 8-18 %
-// slower than kind 4, profiles/r3_rejected_persistent_prefill_gemm.log (compiler-inserted vmcnt(0)
-// before the epilogue's global loads also wait for the previous pass's stores).
-constexpr int PP_CT_BYTES = 64 * 128 * 4;        // 32 KiB fp32 C slice
-constexpr int PP_SMEM = P8_SMEM + PP_CT_BYTES;   // 160 KiB
-
-template <int EPI>
-__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m, int tiles_n, int G) {
-  __shared__ __attribute__((aligned(16))) char smem[PP_SMEM];
-  const int total = tiles_m * tiles_n;
-  const int nb = (int)gridDim.x, b0 = (int)blockIdx.x;
-  const int ntile = (total - b0 + nb - 1) / nb;
-  const int T = p.K / 64;
-  const int U = ntile * T;
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int wr = w >> 2, wc = w & 3;
-  const int r = lane & 15, g = lane >> 4;
-
-  auto tile_of = [&](int j, int& m0, int& n0) {
-    int tm, tn;
-    tile_order(xcd_remap(b0 + j * nb, total), tiles_m, tiles_n, G, tm, tn);
-    m0 = tm * 256;
-    n0 = tn * 256;
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // half h (0 = A0, 1 = A1, 2 = B0, 3 = B1) of the k-tile at k0 of the tile at
-  // (m0, n0) into LDS buffer `buf`; the stream position is tracked by the loop
-  // (current tile, next tile, k-tile index) instead of dividing u by T per call
-  auto stage = [&](int buf, int m0, int n0, int k0, int h) {
-    char* dst = smem + buf * P8_BUF + h * P8_HALF;
-    if (h < 2) p8_stage<true>(dst, p.A, p.lda, m0 + h * 128, p.M - 1, k0);
-    else p8_stage<true>(dst, p.W, p.ldw, n0 + (h - 2) * 128, p.N - 1, k0);
-  };
-  bf16x8 af[4][2], b0f[2][2], b1f[2][2];
-  auto read_a = [&](int u, int mh) {
-    const char* src = smem + (u & 1) * P8_BUF + mh * P8_HALF;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = lds_frag(src, wr * 64 + i * 16 + r, kk * 4 + g);
-  };
-  auto read_b = [&](int u, int nh, bf16x8 (&bf)[2][2]) {
-    const char* src = smem + (u & 1) * P8_BUF + (2 + nh) * P8_HALF;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = lds_frag(src, wc * 32 + j * 16 + r, kk * 4 + g);
-  };
-  auto mma = [&](int mh, int nh, bf16x8 (&bf)[2][2]) {
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_waitcnt(LGKM0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[mh * 4 + i][nh * 2 + j] = mfma16(af[i][kk], bf[j][kk], acc[mh * 4 + i][nh * 2 + j]);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-  };
-  float* ct = reinterpret_cast<float*>(smem + P8_SMEM);
-  auto epilogue = [&](int m0, int n0) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int mh = e >> 2, nh = (e >> 1) & 1, i2 = e & 1;
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int row = wr * 32 + ii * 16 + 4 * g + q;
-            const int col = wc * 32 + jj * 16 + r;
-            ct[row * 128 + (col ^ (((row >> 2) & 3) << 4))] = acc[mh * 4 + i2 * 2 + ii][nh * 2 + jj][q];
-          }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if constexpr (EPI != EPI_SILU_MUL) {
-        store_pass<EPI, 2, 512>(p, 64 * 16, 0, [&](int c, int& m, int& n, const float*& src) {
-          const int row = c >> 4, ch = c & 15;
-          m = m0 + mh * 128 + (row >> 5) * 64 + i2 * 32 + (row & 31);
-          n = n0 + nh * 128 + ch * 8;
-          src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
-          return m < p.M && n < p.N;
-        });
-      }
-#pragma unroll
-      for (int c0 = 0; c0 < 2; ++c0) {
-        if constexpr (EPI != EPI_SILU_MUL) break;
-        const int c = (int)threadIdx.x + c0 * 512;
-        const int row = c >> 4, ch = c & 15;
-        const int m = m0 + mh * 128 + (row >> 5) * 64 + i2 * 32 + (row & 31);
-        const int n = n0 + nh * 128 + ch * 8;
-        if (m >= p.M || n >= p.N) continue;
-        const float* src = ct + row * 128 + ((ch * 8) ^ (((row >> 2) & 3) << 4));
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
-        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if constexpr (EPI == EPI_SILU_MUL) {
-          if ((ch & 3) >= 2) continue;  // up chunks are read by their gate chunk
-          const float* up = ct + row * 128 + (((ch + 2) * 8) ^ (((row >> 2) & 3) << 4));
-          const f32x4 ulo = *reinterpret_cast<const f32x4*>(up);
-          const f32x4 uhi = *reinterpret_cast<const f32x4*>(up + 4);
-          const float uu[8] = {ulo[0], ulo[1], ulo[2], ulo[3], uhi[0], uhi[1], uhi[2], uhi[3]};
-          bf16x8 o;
-#pragma unroll
-          for (int x = 0; x < 8; ++x) o[x] = f2bf(silu(v[x]) * uu[x]);
-          st8(reinterpret_cast<bf16*>(p.out) + (long)m * p.ldo + (n >> 5) * 16 + (n & 15), o);
-        } else {
-          epilogue8<EPI>(p, m, n, v, 0);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // slice read before the next pass overwrites it
-    }
-  };
-
-  if (U > 0) {
-    int cm0, cn0, xm0 = 0, xn0 = 0;  // current tile, next tile
-    tile_of(0, cm0, cn0);
-    if (ntile > 1) tile_of(1, xm0, xn0);
-    stage(0, cm0, cn0, 0, 0);
-    stage(0, cm0, cn0, 0, 2);
-    stage(0, cm0, cn0, 0, 3);
-    stage(0, cm0, cn0, 0, 1);
-    if (U > 1) {  // k-tile 1 of the stream: this tile's (T >= 2: host-checked)
-      stage(1, cm0, cn0, 64, 0);
-      stage(1, cm0, cn0, 64, 2);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
-
-    int kt = 0, j = 0;
-    for (int t = 0; t < U; ++t) {
-      const bool n1 = t + 1 < U, n2 = t + 2 < U;
-      // stream k-tiles t + 1 and t + 2: (tile, k0)
-      const bool s1 = kt + 1 < T, s2 = kt + 2 < T;
-      const int m1 = s1 ? cm0 : xm0, c1 = s1 ? cn0 : xn0, k1 = s1 ? (kt + 1) * 64 : 0;
-      const int m2 = s2 ? cm0 : xm0, c2 = s2 ? cn0 : xn0, k2 = s2 ? (kt + 2) * 64 : (kt + 2 - T) * 64;
-      const int bq = (t + 1) & 1, bt = t & 1;
-      // q0: (A0, B0)
-      read_a(t, 0);
-      read_b(t, 0, b0f);
-      if (n1) stage(bq, m1, c1, k1, 3);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(0, 0, b0f);
-      // q1: (A0, B1); retire A1(t)
-      read_b(t, 1, b1f);
-      if (n1) stage(bq, m1, c1, k1, 1);
-      if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      mma(0, 1, b1f);
-      // q2: (A1, B1)
-      read_a(t, 1);
-      if (n2) stage(bt, m2, c2, k2, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(1, 1, b1f);
-      // q3: (A1, B0); retire A0 / B0 / B1 of t + 1
-      if (n2) stage(bt, m2, c2, k2, 2);
-      if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if (n1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      mma(1, 0, b0f);
-      if (++kt == T) {  // tile j done: de-stagger, epilogue, re-stagger
-        if (wr == 0) __builtin_amdgcn_s_barrier();
-        epilogue(cm0, cn0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (wr == 1 && n1) __builtin_amdgcn_s_barrier();
-        kt = 0;
-        ++j;
-        cm0 = xm0;
-        cn0 = xn0;
-        if (j + 1 < ntile) tile_of(j + 1, xm0, xn0);
-      }
-    }
-  }
-}
+// Measured and removed this round (code in git history, commits 312c1a1 / 4bb62e9 / 0c5def8):
+// a persistent one-k-tile-stream variant of the kernel above, one-wave-per-SIMD 4 x 128x128
+// kernels on 16x16x32 and 32x32x16 MFMAs, and a peeled k-loop -- 8-30 % slower or within noise
+// (profiles/r3_rejected_persistent_prefill_gemm.log, r3_rejected_one_wave_per_simd_gemm.log,
+// r3_rejected_p8_peeled_loop.log).
 
 // ---------------------------------------------------------------------------
 // Decode GEMM at 129-256 rows: every row in ONE 256 x BN tile, 8 waves
@@ -2434,9 +1827,9 @@ static int g_big_min_blocks = 160;  // lsd_gemm_set_big_min(): tuning / tests
 // GEMMs 10-25 % faster than M-fastest, 8 equal, 16+ slower
 // (profiles/r2_prefill_tile_order.log)
 static int g_big_group = 4;
-// lsd_gemm_set_big_kind(): 0 = BK=32 ring kernel (gemm_big), 1 = phase-pipelined BK=64 (gemm_p8),
-// 2..5 = gemm_p8 VAR 1..5 (4, the default: buffer_load ... lds staging, +6 % on the GPT-2 XL prefill
-// projections and +25 % at 4096^3 over kind 1; profiles/r3_p8_buffer_lds.log)
+// lsd_gemm_set_big_kind(): 0 = BK=32 ring kernel (gemm_big), 1 = phase-pipelined BK=64 (gemm_p8)
+// with global_load_lds, 4 (default) = the same with buffer_load ... lds staging (+6 % on the GPT-2 XL
+// prefill projections and +25 % at 4096^3 over kind 1; profiles/r3_p8_buffer_lds.log)
 static int g_big_kind = 4;
 // 128x128 launches of at most this many workgroups use the 3-slot ring kernel
 // (1 block/CU); larger grids keep the 2-blocks/CU double-buffered one.
@@ -2543,20 +1936,6 @@ static hipError_t launch_d256(const GemmParams& p, int kind, int* cnt, float* ws
   return bn == 128 ? launch_d256_bn<EPI, 128>(p, cnt, ws, st) : launch_d256_bn<EPI, 64>(p, cnt, ws, st);
 }
 
-// persistent prefill GEMM grid: the CU count rounded down to a multiple of 8
-// (every workgroup keeps one XCD), 1 workgroup per CU (160 KiB LDS)
-static int pp_grid() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8)
-      cus = 256;
-    n = cus / 8 * 8;
-  }
-  return n;
-}
-
 template <int EPI>
 static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
   // 256x256 pipelined kernel once the problem fills the chip with 1-block/CU
@@ -2564,32 +1943,9 @@ static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStre
   const int bm = (p.M + GBM - 1) / GBM, bn = (p.N + GBN - 1) / GBN;
   if (p.M >= GBM && p.K % 64 == 0 && bm * bn * p.splits >= g_big_min_blocks) {
     if (g_big_kind == 1)
-      hipLaunchKernelGGL((gemm_p8_kernel<EPI>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
-                         g_big_group);
-    else if (g_big_kind == 2)
-      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 1>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
-                         g_big_group);
-    else if (g_big_kind == 3)
-      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 3>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
+      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 0>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
                          g_big_group);
     else if (g_big_kind == 4)
-      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 4>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
-                         g_big_group);
-    else if (g_big_kind == 5)
-      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 5>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
-                         g_big_group);
-    else if (g_big_kind == 10)
-      hipLaunchKernelGGL((gemm_p8_kernel<EPI, 12>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
-                         g_big_group);
-    else if (g_big_kind == 9 && p.splits == 1)
-      hipLaunchKernelGGL((gemm_w5_kernel<EPI, 1>), dim3(bm * bn), dim3(256), 0, st, p, bm, bn, g_big_group);
-    else if (g_big_kind == 8 && p.splits == 1)
-      hipLaunchKernelGGL((gemm_w5_kernel<EPI>), dim3(bm * bn), dim3(256), 0, st, p, bm, bn, g_big_group);
-    else if (g_big_kind == 7 && p.splits == 1)
-      hipLaunchKernelGGL((gemm_w4_kernel<EPI>), dim3(bm * bn), dim3(256), 0, st, p, bm, bn, g_big_group);
-    else if (g_big_kind == 6 && p.splits == 1 && p.K >= 128 && bm * bn >= pp_grid())
-      hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(pp_grid()), dim3(512), 0, st, p, bm, bn, g_big_group);
-    else if (g_big_kind == 6)
       hipLaunchKernelGGL((gemm_p8_kernel<EPI, 4>), dim3(bm * bn * p.splits), dim3(512), 0, st, p, bm, bn,
                          g_big_group);
     else
@@ -2670,7 +2026,7 @@ using namespace lsd;
 
 extern "C" void lsd_gemm_set_big_min(int v) { g_big_min_blocks = v; }
 extern "C" void lsd_gemm_set_big_group(int v) { g_big_group = v < 0 ? 0 : v; }
-extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v >= 0 && v <= 10) ? v : 0; }
+extern "C" void lsd_gemm_set_big_kind(int v) { g_big_kind = (v == 1 || v == 4) ? v : 0; }
 extern "C" void lsd_gemm_set_tiled3_max(int v) { g_tiled3_max_blocks = v; }
 extern "C" void lsd_gemm_set_ring_slots(int v) { g_ring_slots = v == 4 ? 4 : 3; }
 extern "C" void lsd_gemm_set_ring_tn(int v) { g_ring_tn = (v == 64 || v == 32 || v == 0) ? v : 128; }

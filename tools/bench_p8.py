@@ -4,7 +4,7 @@
 Shapes: the GPT-2 XL / Llama-3 8B prefill projections at 64K / 8K tokens and the square
 4096^3 / 8192^3 reference points of the guide's 256^2 8-phase template, plain bf16 output
 (EPI none) and the fused epilogue each projection runs in the engine.
-Usage: python tools/bench_p8.py [kind ...]   (kind: value for C.gemm_set_big_kind, default 4)
+Usage: python tools/bench_p8.py [kind ...]   (kind: C.gemm_set_big_kind value 0, 1 or 4; default 4)
 """
 from __future__ import annotations
 
