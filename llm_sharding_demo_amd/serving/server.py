@@ -33,6 +33,7 @@ import torch
 from pydantic import BaseModel
 
 from ..config import EngineConfig, SamplingParams
+from ..utils import racecheck
 from ..utils.metrics import Metrics
 from ..utils.tokenizer import load_tokenizer
 
@@ -76,7 +77,7 @@ class ShardRunner:
                                 weights_path=cfg.weights, max_slots=1,
                                 max_seq=min(cfg.max_seq_len, mc.max_positions))
         self.role = role
-        self.lock = __import__("threading").Lock()
+        self.lock = racecheck.Lock("shard_runner")
 
     def run(self, x: torch.Tensor, seq_len: int) -> torch.Tensor:
         from ..runtime.batch import BatchMeta

@@ -9,10 +9,11 @@ percentiles from the engine's hipEvent step timings.
 """
 from __future__ import annotations
 
-import threading
 import time
 from collections import deque
 from typing import Dict, Iterable, Optional
+
+from . import racecheck
 
 
 def percentile(xs, q: float) -> float:
@@ -24,9 +25,9 @@ def percentile(xs, q: float) -> float:
     return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
 
 
-class Metrics:
+class Metrics(racecheck.Shared):
     def __init__(self, window: int = 4096, rate_window_s: float = 60.0):
-        self._lock = threading.Lock()
+        self._lock = racecheck.Lock("metrics")
         self.requests = 0
         self.tokens = 0
         self.t0 = time.monotonic()
@@ -41,6 +42,7 @@ class Metrics:
     def observe_request(self, n_tokens: int, seconds: float, ttft_s: Optional[float] = None) -> None:
         now = time.monotonic()
         with self._lock:
+            racecheck.note(self, "_done")
             self.requests += 1
             self.tokens += n_tokens
             self.request_s.append(seconds)
@@ -57,6 +59,7 @@ class Metrics:
             if key is not None and key == self._last_steps_key:
                 return  # the same session's steps are only counted once
             self._last_steps_key = key
+            racecheck.note(self, "step_ms")
             self.step_ms.extend(steps_ms)
 
     def tokens_per_second(self) -> float:

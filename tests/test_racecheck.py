@@ -188,3 +188,33 @@ for r in rc.reports():
 print("reports", len(rc.reports()))
 """, timeout=110)
     assert "reports 0" in out, out
+
+
+def test_http_serving_is_race_free():
+    """Concurrent /generate calls through the FastAPI app (handler threads), the
+    serving loop, 2 stage threads, metrics and /metrics + /health readers."""
+    out = _run("""
+import threading
+from fastapi.testclient import TestClient
+from llm_sharding_demo_amd.utils import racecheck as rc
+from llm_sharding_demo_amd.config import EngineConfig
+from llm_sharding_demo_amd.runtime.engine import Engine
+from llm_sharding_demo_amd.serving.server import create_app
+
+cfg = EngineConfig(model_id="gpt2-test", num_stages=2, max_batch=8, device="cpu", metrics_every=1)
+eng = Engine(cfg)
+client = TestClient(create_app(cfg, engine=eng))
+res = [None] * 8
+def go(i):
+    res[i] = client.post("/generate", json={"prompt": f"hi {i}", "max_new_tokens": 4, "greedy": True}).json()
+    client.get("/metrics"); client.get("/health")
+ts = [threading.Thread(target=go, args=(i,)) for i in range(8)]
+[t.start() for t in ts]; [t.join() for t in ts]
+assert all("generated" in r for r in res), res
+eng.stop_loop()
+for r in rc.reports():
+    print("RACE", r["object"], r["field"], r["thread"], r["held"])
+    print(r["stack"])
+print("reports", len(rc.reports()))
+""")
+    assert "reports 0" in out, out
