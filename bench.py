@@ -51,8 +51,11 @@ def parse():
     p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),
                    help="nccl (RCCL via torch.distributed) | rccl (native RCCL communicator, csrc/comm.cpp) | gloo (host-staged, for rehearsals)")
     p.add_argument("--loopback-stages", type=int, default=0,
-                   help="rehearsal: run this many pipeline stages as threads on ONE GPU "
-                        "(device-async loopback transport); --batch is then the total batch")
+                   help="rehearsal: run this many pipeline stages as threads on ONE GPU; "
+                        "--batch is then the total batch")
+    p.add_argument("--loopback-transport", default=os.environ.get("BENCH_LOOPBACK", "devloop"),
+                   help="devloop (device loopback channels: graph-captured transfers + the native "
+                        "executor, the rccl data plane's code path) | loopback (event hand-off)")
     p.add_argument("--prefill-chunk", type=int, default=int(os.environ.get("BENCH_PREFILL_CHUNK", "-1")),
                    help="prompt tokens per prefill chunk (0: whole prompts); -1 -> auto: whole prompts on "
                         "one stage, prompt/4 (>= 32) on P >= 2 stages.  Chunks shorten the pipeline fill "
@@ -114,7 +117,7 @@ def main() -> int:
             raise SystemExit("--loopback-stages runs on one GPU")
         P = args.loopback_stages
         M = args.microbatches or auto_groups(args, P)
-        transport = "loopback"
+        transport = args.loopback_transport
     chunk = args.prefill_chunk
     if chunk < 0:
         chunk = 0 if P == 1 else max(32, args.prompt // 4)

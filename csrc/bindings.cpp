@@ -601,11 +601,13 @@ void sample_into(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Ten
 
 void lsd_register_comm(pybind11::module& m);  // csrc/comm.cpp
 void lsd_register_exec(pybind11::module& m);  // csrc/stage_exec.cpp
+void lsd_register_loopback(pybind11::module& m);  // csrc/loop_fabric.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "CDNA4 (gfx950) kernels for llm_sharding_demo_amd";
   lsd_register_comm(m);
   lsd_register_exec(m);
+  lsd_register_loopback(m);
   m.def("linear", &linear);
   m.def("linear_f32", &linear_f32);
   m.def("linear_residual", &linear_residual);

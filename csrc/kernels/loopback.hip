@@ -1,0 +1,196 @@
+// Device-side loopback channels: the RCCL-shaped data plane of the
+// single-GPU pipeline rehearsal (parallel/comm.py DeviceLoopTransport).
+//
+// The reference relays every hidden state through its coordinator over HTTP
+// (`server.py:171-181`).  On an 8-GPU node a pipeline edge is an RCCL
+// ncclSend / ncclRecv pair on a 2-rank communicator whose kernels spin on a
+// FIFO of slots in the peer's memory.  On ONE MI355X the rehearsal needs the
+// same semantics -- ops enqueued on the lane stream (eagerly or captured in a
+// hipGraph), matched strictly in per-channel FIFO order, device-side waits,
+// no host synchronisation -- so a channel here is that FIFO: a byte ring in
+// HBM plus a ring of message headers, written by the sending stage's kernels
+// and drained by the receiving stage's.
+//
+// Protocol (one channel = one (edge, lane) of one pipeline):
+//   send  = copy kernel (every block: wait for ring space, copy its part) +
+//           publish kernel (1 wave: header {size, offset}, tag = seq + 1)
+//   recv  = copy kernel (every block: wait for tag, check size, copy out) +
+//           release kernel (1 wave: advance the consumed offset / sequence)
+// The two kernels of an op are stream-ordered, so a kernel boundary orders
+// the payload before its publish and the reads before the release.  Every
+// cross-stream word is an agent-scope atomic (tags / consumed counters),
+// every wait is polled by ONE lane per block, bounded in time (s_memrealtime)
+// and abortable through a word in pinned host memory (the watchdog's abort):
+// no spin in this file can outlive its deadline.
+//
+// Header size check: a receive whose posted size differs from the message at
+// the head of its channel records LOOP_ERR_MISMATCH instead of copying -- the
+// RCCL op-ordering contract (same op sequence on both ends of a communicator)
+// checked on every transfer.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "loopback.h"
+
+namespace {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+constexpr int THREADS = 256;
+constexpr int CHUNK = THREADS * 16 * 4;  // bytes per block per pass (4 x 16 B per thread)
+
+__device__ __forceinline__ u64 ld_agent(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent_release(u64* p, u64 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u32 ld_sys(const u32* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void set_err(LoopStatus* st, u32 code, u32 chan) {
+  // vector stores to the pinned status block (first error is enough; a
+  // later one may overwrite it -- any non-zero code fails the engine)
+  __hip_atomic_store(&st->err_chan, chan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&st->err, code, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Ring placement: a message occupies [off, off + bytes) of the monotonic byte
+// stream and never straddles the ring's end (it skips to the next lap).
+__device__ __host__ __forceinline__ u64 place(u64 head, u64 bytes, u64 cap) {
+  const u64 o = head % cap;
+  return (o + bytes > cap) ? head + (cap - o) : head;
+}
+
+// Bounded wait helper: ONE lane polls; every 64 polls it also reads the
+// host abort word.  Returns 0 (condition met), LOOP_ERR_ABORT or
+// LOOP_ERR_TIMEOUT.
+template <typename Cond>
+__device__ u32 bounded_wait(Cond cond, const LoopStatus* st, u64 limit_ticks) {
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  for (u32 n = 0;; ++n) {
+    if (cond()) return 0;
+    if ((n & 63) == 63) {
+      if (ld_sys(&st->abort)) return LOOP_ERR_ABORT;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > limit_ticks) return LOOP_ERR_TIMEOUT;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// 16-byte vector copy of [0, bytes) when both ends are 16-B aligned, 4-byte
+// words otherwise (every wire tensor is fp32 / bf16 / int32: sizes % 2 == 0;
+// a trailing odd half-word is copied bytewise).
+__device__ __forceinline__ void copy_part(uint8_t* dst, const uint8_t* src, u64 bytes) {
+  const u64 tid = (u64)blockIdx.x * THREADS + threadIdx.x;
+  const u64 nth = (u64)gridDim.x * THREADS;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+    const u64 n16 = bytes >> 4;
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (u64 i = tid; i < n16; i += nth) d[i] = s[i];
+    for (u64 i = (n16 << 4) + tid; i < bytes; i += nth) dst[i] = src[i];
+  } else if ((((uintptr_t)dst | (uintptr_t)src) & 3) == 0) {
+    const u64 n4 = bytes >> 2;
+    const u32* s = reinterpret_cast<const u32*>(src);
+    u32* d = reinterpret_cast<u32*>(dst);
+    for (u64 i = tid; i < n4; i += nth) d[i] = s[i];
+    for (u64 i = (n4 << 2) + tid; i < bytes; i += nth) dst[i] = src[i];
+  } else {
+    for (u64 i = tid; i < bytes; i += nth) dst[i] = src[i];
+  }
+}
+
+__global__ __launch_bounds__(THREADS) void loop_send_copy(LoopChan* ch, const uint8_t* src, u64 bytes,
+                                                          LoopStatus* st) {
+  __shared__ u32 verdict;
+  const u64 cap = ch->cap, nh = LOOP_HEADERS;
+  const u64 seq = ch->s_seq, head = ch->s_off;  // sender-private: stream-ordered
+  const u64 off = place(head, bytes, cap);
+  if (threadIdx.x == 0) {
+    verdict = bounded_wait(
+        [&] {
+          // header slot free and [r_off, off + bytes) within one ring
+          return seq - ld_agent(&ch->r_seq) < nh && off + bytes - ld_agent(&ch->r_off) <= cap;
+        },
+        st, ch->spin_limit);
+    if (verdict) set_err(st, verdict, ch->id);
+  }
+  __syncthreads();
+  if (verdict) return;
+  copy_part(ch->ring + off % cap, src, bytes);
+}
+
+__global__ void loop_send_publish(LoopChan* ch, u64 bytes) {
+  if (threadIdx.x != 0) return;
+  const u64 cap = ch->cap;
+  const u64 seq = ch->s_seq, off = place(ch->s_off, bytes, cap);
+  const u32 k = (u32)(seq % LOOP_HEADERS);
+  __hip_atomic_store(&ch->h_size[k], bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&ch->h_off[k], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  st_agent_release(&ch->h_tag[k], seq + 1);  // the payload (previous kernel) and header before the tag
+  ch->s_seq = seq + 1;
+  ch->s_off = off + bytes;
+}
+
+__global__ __launch_bounds__(THREADS) void loop_recv_copy(LoopChan* ch, uint8_t* dst, u64 bytes,
+                                                          LoopStatus* st) {
+  __shared__ u32 verdict;
+  __shared__ u64 s_off;
+  const u64 seq = ch->r_seq;  // receiver-private: stream-ordered
+  const u32 k = (u32)(seq % LOOP_HEADERS);
+  if (threadIdx.x == 0) {
+    u32 v = bounded_wait([&] { return ld_agent(&ch->h_tag[k]) == seq + 1; }, st, ch->spin_limit);
+    if (!v) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const u64 sz = ld_agent(&ch->h_size[k]);
+      s_off = ld_agent(&ch->h_off[k]);
+      if (sz != bytes) v = LOOP_ERR_MISMATCH;
+    }
+    if (v) set_err(st, v, ch->id);
+    verdict = v;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (verdict) return;
+  copy_part(dst, ch->ring + s_off % ch->cap, bytes);
+}
+
+__global__ void loop_recv_release(LoopChan* ch) {
+  if (threadIdx.x != 0) return;
+  const u64 seq = ch->r_seq;
+  const u32 k = (u32)(seq % LOOP_HEADERS);
+  if (ld_agent(&ch->h_tag[k]) != seq + 1) return;  // the copy gave up (error already recorded)
+  const u64 end = ld_agent(&ch->h_off[k]) + ld_agent(&ch->h_size[k]);
+  // the copy kernel's reads of the ring completed before this kernel began
+  st_agent_release(&ch->r_off, end);
+  st_agent_release(&ch->r_seq, seq + 1);
+}
+
+int copy_blocks(u64 bytes) {
+  const u64 b = (bytes + CHUNK - 1) / CHUNK;
+  return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
+}
+
+}  // namespace
+
+extern "C" hipError_t lsd_loop_send(LoopChan* ch, const void* src, uint64_t bytes, LoopStatus* st,
+                                    hipStream_t s) {
+  hipLaunchKernelGGL(loop_send_copy, dim3(copy_blocks(bytes)), dim3(THREADS), 0, s, ch,
+                     static_cast<const uint8_t*>(src), bytes, st);
+  hipLaunchKernelGGL(loop_send_publish, dim3(1), dim3(64), 0, s, ch, bytes);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t lsd_loop_recv(LoopChan* ch, void* dst, uint64_t bytes, LoopStatus* st,
+                                    hipStream_t s) {
+  hipLaunchKernelGGL(loop_recv_copy, dim3(copy_blocks(bytes)), dim3(THREADS), 0, s, ch,
+                     static_cast<uint8_t*>(dst), bytes, st);
+  hipLaunchKernelGGL(loop_recv_release, dim3(1), dim3(64), 0, s, ch);
+  return hipGetLastError();
+}
+
+extern "C" uint64_t lsd_loop_place(uint64_t head, uint64_t bytes, uint64_t cap) {
+  return place(head, bytes, cap);
+}

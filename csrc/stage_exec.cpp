@@ -9,11 +9,13 @@
 // own edge send / receive) -- is handed to `exec_items` as a list of plain
 // handles, and the whole step is enqueued here without returning to the
 // interpreter between items.  Per item, in stream order on its lane:
-//   [token-return receive (stage 0 of a multi-stage pipeline, ncclRecv)]
+//   [token-return receive (stage 0 of a multi-stage pipeline, ncclRecv, or a
+//    loopback-channel receive in the single-GPU rehearsal)]
 //   [busy-timing event]
 //   [token readout: D2H copy of the previous item's sampled ids into a pinned
 //    host buffer + completion event the scheduler polls]
-//   hipGraphLaunch of the item's decode graph
+//   hipGraphLaunch of the item's decode graph (its captured loopback ops
+//    pass the enqueue handshake first and advance the host mirrors after)
 //   [busy-timing event]
 // The reference's equivalent is its per-token coordinator loop of two HTTP
 // hops (`server.py:169-206`); here the loop body is one C++ call per step.
@@ -29,6 +31,9 @@
 namespace py = pybind11;
 
 void lsd_rccl_recv_raw(int64_t h, void* ptr, size_t bytes, int peer, hipStream_t st);  // comm.cpp
+void lsd_loop_recv_raw(int64_t chan, void* ptr, size_t bytes, hipStream_t st);          // loop_fabric.cpp
+void lsd_loop_io_wait(int64_t io);
+void lsd_loop_io_done(int64_t io);
 
 namespace {
 
@@ -50,6 +55,8 @@ enum : int {
   X_BYTES,       //   bytes
   X_EV,          //   completion event
   X_T1,          // busy-timing event after the item
+  X_RLOOP,       // token-return receive on a loopback channel (instead of X_RCOMM)
+  X_IO,          // loopback I/O list captured in the graph (enqueue handshake + mirrors)
   X_FIELDS
 };
 
@@ -63,6 +70,7 @@ void lsd_register_exec(py::module& m) {
       if (it[X_RCOMM])
         lsd_rccl_recv_raw(it[X_RCOMM], reinterpret_cast<void*>(it[X_RPTR]), (size_t)it[X_RBYTES],
                           (int)it[X_RPEER], st);
+      if (it[X_RLOOP]) lsd_loop_recv_raw(it[X_RLOOP], reinterpret_cast<void*>(it[X_RPTR]), (size_t)it[X_RBYTES], st);
       if (it[X_T0]) hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(it[X_T0]), st), "hipEventRecord");
       if (it[X_BYTES]) {
         hip_check(hipMemcpyAsync(reinterpret_cast<void*>(it[X_DST]), reinterpret_cast<const void*>(it[X_SRC]),
@@ -71,7 +79,9 @@ void lsd_register_exec(py::module& m) {
         hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(it[X_EV]), st), "hipEventRecord");
       }
       if (!it[X_GRAPH]) throw std::invalid_argument("exec_items: item without a graph");
+      if (it[X_IO]) lsd_loop_io_wait(it[X_IO]);  // instant: the caller pre-waited the step's ops
       hip_check(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(it[X_GRAPH]), st), "hipGraphLaunch");
+      if (it[X_IO]) lsd_loop_io_done(it[X_IO]);
       if (it[X_T1]) hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(it[X_T1]), st), "hipEventRecord");
     }
   }, py::arg("items"));

@@ -233,8 +233,11 @@ class EngineConfig:
     shard_a_service: str = "llm-shard-a"
     shard_b_service: str = "llm-shard-b"
     shard_port: int = 5000
-    # auto | nccl | gloo | local | http | loopback (P stage threads on one GPU,
-    # device-async event hand-off: single-GPU rehearsal of the RCCL schedule)
+    # auto | nccl | rccl | gloo | local | http | loopback (P stage threads on
+    # one GPU, device-async event hand-off) | devloop (P stage threads on one
+    # GPU joined by device loopback channels with graph-captured transfers:
+    # the single-GPU rehearsal of the rccl data plane) | strict (host queues
+    # per (edge, lane) with receive-size checks: CPU protocol tests)
     transport: str = "auto"
     # Boundary hidden states on the wire: "fp32" (the residual stream as is:
     # bit-identical to one stage) or "bf16" (half the bytes per hop; the

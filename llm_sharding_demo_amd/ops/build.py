@@ -27,9 +27,10 @@ BUILD = os.path.join(ROOT, "build", "native")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-KERNELS = ["gemm.hip", "gemv.hip", "norm.hip", "attention.hip", "sample.hip"]
-# host code of the extension: kernel bindings, native RCCL communicator, native stage executor
-HOST_SOURCES = ["bindings.cpp", "comm.cpp", "stage_exec.cpp"]
+KERNELS = ["gemm.hip", "gemv.hip", "norm.hip", "attention.hip", "sample.hip", "loopback.hip"]
+# host code of the extension: kernel bindings, native RCCL communicator, native stage
+# executor, device loopback channels (single-GPU rehearsal of the RCCL edges)
+HOST_SOURCES = ["bindings.cpp", "comm.cpp", "stage_exec.cpp", "loop_fabric.cpp"]
 EXT_NAME = "_C"
 
 

@@ -31,6 +31,7 @@ owes on an earlier item.
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import pickle
 import queue
@@ -91,6 +92,12 @@ class Transport:
 
     def abort(self) -> None:
         """Unblock anything waiting on the data plane (native RCCL only)."""
+
+    def issuing(self):
+        """Context of a data-plane enqueue that bypasses send / irecv (a graph
+        replay with captured transfers, the native executor): the native RCCL
+        transport holds its abort gate shared across it."""
+        return contextlib.nullcontext()
 
     def broadcast_object(self, obj, src: int = 0):
         raise NotImplementedError
@@ -305,6 +312,13 @@ class RcclTransport(_DistTransport):
         self.comms: Dict[tuple, tuple] = {}  # (edge group name, lane) -> (handle, my index)
         self.aborted = False
         self._lock = threading.Lock()
+        # abort gate: every enqueue that touches a communicator runs between
+        # _enter / _exit; abort() flips `aborted` (no new enqueue starts), then
+        # waits for the enqueues in flight before ncclCommAbort frees the
+        # communicators (bounded: an enqueue stuck behind a hung GPU must not
+        # keep the abort that would unstick it from running)
+        self._issue = threading.Condition()
+        self._inflight = 0
         for name in self.groups:
             members = self._members(name)
             for lane in range(self.L):
@@ -324,22 +338,41 @@ class RcclTransport(_DistTransport):
             raise TransportError(f"RCCL communicators aborted; {edge} edge unusable")
         return self.comms[(name, lane % self.L)]
 
+    @contextlib.contextmanager
+    def issuing(self):
+        with self._issue:
+            if self.aborted:
+                raise TransportError("RCCL communicators aborted")
+            self._inflight += 1
+        try:
+            yield
+        finally:
+            with self._issue:
+                self._inflight -= 1
+                self._issue.notify_all()
+
     def send(self, t, dst, edge, lane: int = 0):
-        h, me = self._edge(edge, self.rank, dst, lane)
         if not t.is_contiguous():
             t = t.contiguous()
-        self.C.rccl_send(h, t, 1 - me)
+        with self.issuing():
+            h, me = self._edge(edge, self.rank, dst, lane)
+            self.C.rccl_send(h, t, 1 - me)
         t.record_stream(torch.cuda.current_stream())
         return SendHandle()
 
     def irecv(self, out, src, edge, lane: int = 0):
-        h, me = self._edge(edge, src, self.rank, lane)
-        if out.is_contiguous():
-            self.C.rccl_recv(h, out, 1 - me)
+        buf = out if out.is_contiguous() else torch.empty(out.shape, dtype=out.dtype, device=out.device)
+        with self.issuing():
+            h, me = self._edge(edge, src, self.rank, lane)
+            self.C.rccl_recv(h, buf, 1 - me)
+        if buf is out:
             return Handle(out)
-        buf = torch.empty(out.shape, dtype=out.dtype, device=out.device)
-        self.C.rccl_recv(h, buf, 1 - me)
         return Handle(out, post=lambda: out.copy_(buf))
+
+    def native_recv(self, edge: str, src: int, lane: int) -> tuple:
+        """("rccl", communicator, peer) of a receive the native executor enqueues."""
+        h, me = self._edge(edge, src, self.rank, lane)
+        return ("rccl", h, 1 - me)
 
     # graph capture: the same enqueue on the capture stream
     capture_send = send
@@ -369,7 +402,7 @@ class RcclTransport(_DistTransport):
     def check_async(self) -> Optional[str]:
         """First asynchronous RCCL error of any communicator, or None."""
         with self._lock:
-            if self.aborted:
+            if self.aborted or getattr(self, "_comms_aborted", False):
                 return None
             for (name, lane), (h, _) in self.comms.items():
                 e = self.C.rccl_async_error(h)
@@ -377,12 +410,19 @@ class RcclTransport(_DistTransport):
                     return f"RCCL {name}/lane{lane}: {self.C.rccl_error_string(e)}"
         return None
 
-    def abort(self) -> None:
-        """Abort every communicator (unblocks kernels waiting on a peer)."""
-        with self._lock:
-            if self.aborted:
-                return
+    def abort(self, drain_s: float = 5.0) -> None:
+        """Abort every communicator (unblocks kernels waiting on a peer).
+        New enqueues are refused first; enqueues already inside an RCCL call
+        get up to `drain_s` to leave it before the communicators are freed."""
+        with self._issue:
             self.aborted = True
+            deadline = time.monotonic() + drain_s
+            while self._inflight and time.monotonic() < deadline:
+                self._issue.wait(0.05)
+        with self._lock:
+            if getattr(self, "_comms_aborted", False):
+                return
+            self._comms_aborted = True
             for h, _ in self.comms.values():
                 try:
                     self.C.rccl_comm_abort(h)
@@ -503,7 +543,11 @@ class LocalFabric(racecheck.Shared):
             return n
 
     def transport(self, rank: int, kind: str = "local") -> Transport:
-        return LoopbackTransport(self, rank) if kind == "loopback" else LocalTransport(self, rank)
+        if kind == "loopback":
+            return LoopbackTransport(self, rank)
+        if kind == "strict":
+            return StrictLocalTransport(self, rank)
+        return LocalTransport(self, rank)
 
 
 class LoopbackTransport(Transport):
@@ -552,6 +596,189 @@ class LoopbackTransport(Transport):
         self.fabric._barrier.wait(timeout=self.fabric.timeout)
 
 
+class DeviceLoopFabric(LocalFabric):
+    """P in-process stages on ONE MI355X joined by device loopback channels
+    (csrc/kernels/loopback.hip, csrc/loop_fabric.cpp): the single-GPU
+    rehearsal of the RCCL data plane, graph I/O included.
+
+    One channel per (edge, lane) -- forward edges i -> i+1 and the token
+    return P-1 -> 0, times the L lane streams -- exactly the communicator
+    layout of `RcclTransport`, with the same contract: ops of a channel are
+    matched in FIFO order, so both ends must issue them in the same order.
+    Every receive checks the size of the message at its channel's head on
+    the device and records a mismatch instead of copying, so the rehearsal
+    verifies RCCL's op-ordering contract on every transfer.
+
+    Ring sizing: a message must fit its channel's ring (`ring_bytes` for the
+    forward edges, `ret_bytes` for the token return); both are allocated up
+    front, before the KV cache takes its share of HBM."""
+
+    def __init__(self, num_stages: int, device: torch.device, lanes: int, ring_bytes: int,
+                 ret_bytes: int = 16 << 20, timeout: float = 60.0, spin_limit_s: float = 30.0):
+        super().__init__(num_stages, timeout=timeout)
+        from ..ops.hip import _load
+
+        self.C = _load()
+        self.L = max(1, lanes)
+        self.device = device
+        self.handle = self.C.loop_fabric_create(float(timeout))
+        self._keep: List[torch.Tensor] = []
+        self.chans: Dict[tuple, int] = {}
+        nstate = self.C.loop_state_bytes()
+        edges = [("fwd", i, i + 1) for i in range(num_stages - 1)]
+        if num_stages > 1:
+            edges.append(("ret", num_stages - 1, 0))
+        with torch.cuda.device(device):
+            for edge, src, dst in edges:
+                nbytes = ring_bytes if edge == "fwd" else ret_bytes
+                nbytes = -(-nbytes // 256) * 256
+                for lane in range(self.L):
+                    state = torch.zeros(nstate, dtype=torch.uint8, device=device)
+                    ring = torch.empty(nbytes, dtype=torch.uint8, device=device)
+                    self._keep += [state, ring]
+                    self.chans[(edge, src, dst, lane)] = self.C.loop_chan_create(
+                        self.handle, state, ring, float(spin_limit_s))
+            torch.cuda.synchronize(device)
+        self.aborted = False
+
+    def transport(self, rank: int, kind: str = "devloop") -> Transport:
+        return DeviceLoopTransport(self, rank)
+
+    def chan(self, edge: str, src: int, dst: int, lane: int) -> int:
+        return self.chans[(edge, src, dst, lane % self.L)]
+
+    # data-plane health (runtime/scheduler.py Watchdog)
+    def check_async(self) -> Optional[str]:
+        err, ch = self.C.loop_status(self.handle)
+        if err == 0 or self.aborted:
+            return None
+        keys = list(self.chans)  # creation order = channel id
+        what = {1: "aborted", 2: "device wait timed out",
+                3: "receive size != message size (op order mismatch)"}
+        key = keys[ch] if 0 <= ch < len(keys) else ch
+        return f"loopback channel {key}: {what.get(err, f'error {err}')}"
+
+    def abort(self) -> None:
+        """Make every waiting kernel and host handshake give up (the RCCL
+        transport's ncclCommAbort)."""
+        self.aborted = True
+        self.C.loop_abort(self.handle)
+
+    def stall(self, edge: str, src: int, dst: int, lane: int, from_msg: int) -> None:
+        """Fault injection: sends number >= from_msg on this channel are never
+        published (the receiver's kernel waits on the device)."""
+        self.C.loop_stall(self.chan(edge, src, dst, lane), from_msg)
+
+    def counts(self, edge: str, src: int, dst: int, lane: int) -> tuple:
+        """(sends enqueued, receives enqueued, send bytes end, recv bytes end)."""
+        return tuple(self.C.loop_counts(self.chan(edge, src, dst, lane)))
+
+
+class DeviceLoopTransport(Transport):
+    """One stage's view of a `DeviceLoopFabric`: the API of `RcclTransport`
+    (ops enqueued on the current stream, eagerly or inside a hipGraph
+    capture; handles already complete in stream order), so the pipeline
+    takes its graph-I/O path and the native executor exactly as over RCCL."""
+
+    GRAPH_IO = True
+
+    def __init__(self, fabric: DeviceLoopFabric, rank: int):
+        self.fabric, self.rank, self.world = fabric, rank, fabric.P
+        self.C = fabric.C
+        self._tls = threading.local()
+
+    @property
+    def aborted(self) -> bool:
+        return self.fabric.aborted
+
+    def _op(self, ch: int, d: int, t: torch.Tensor) -> None:
+        from .pipeline import GPU_GATE
+
+        if self.fabric.aborted:
+            raise TransportError("loopback data plane aborted")
+        nbytes = t.numel() * t.element_size()
+        ops = getattr(self._tls, "ops", None)
+        if ops is not None and torch.cuda.is_current_stream_capturing():
+            (self.C.loop_recv if d else self.C.loop_send)(ch, t, True)
+            ops.append((ch, d, nbytes))
+            return
+        try:
+            with GPU_GATE.released():  # the peer may need the gate to reach its enqueue
+                self.C.loop_wait([(ch, d, nbytes)])
+            with GPU_GATE.shared():
+                (self.C.loop_recv if d else self.C.loop_send)(ch, t, False)
+        except RuntimeError as e:
+            raise TransportError(str(e)) from e
+
+    def send(self, t, dst, edge, lane=0):
+        if not t.is_contiguous():
+            t = t.contiguous()
+        self._op(self.fabric.chan(edge, self.rank, dst, lane), 0, t)
+        return SendHandle()
+
+    def irecv(self, out, src, edge, lane=0):
+        ch = self.fabric.chan(edge, src, self.rank, lane)
+        if out.is_contiguous():
+            self._op(ch, 1, out)
+            return Handle(out)
+        buf = torch.empty(out.shape, dtype=out.dtype, device=out.device)
+        self._op(ch, 1, buf)
+        return Handle(out, post=lambda: out.copy_(buf))
+
+    capture_send = send
+    capture_recv = irecv
+
+    # -- graph I/O: ops captured inside a decode graph ----------------------
+    def begin_capture(self) -> None:
+        self._tls.ops = []
+
+    def end_capture(self) -> tuple:
+        """(native I/O-list handle or 0, op list) of the capture just ended."""
+        ops = self._tls.ops
+        self._tls.ops = None
+        return (self.C.loop_io_create(ops) if ops else 0), ops
+
+    def prewait(self, ops: List[tuple]) -> None:
+        """Enqueue handshake of (chan, dir, bytes) ops about to be issued,
+        outside the capture gate (the step's ops in the native executor)."""
+        from .pipeline import GPU_GATE
+
+        if self.fabric.aborted:
+            raise TransportError("loopback data plane aborted")
+        if not ops:
+            return
+        try:
+            with GPU_GATE.released():
+                self.C.loop_wait(ops)
+        except RuntimeError as e:
+            raise TransportError(str(e)) from e
+
+    def replay(self, g, io: int, ops: List[tuple]) -> None:
+        """Launch a decode graph whose loopback ops are `io` on the current
+        stream: handshake (gate released), launch, advance the mirrors."""
+        self.prewait(ops)
+        try:
+            self.C.loop_graph_launch(g.raw_cuda_graph_exec(), io)
+        except RuntimeError as e:
+            raise TransportError(str(e)) from e
+
+    def native_recv(self, edge: str, src: int, lane: int) -> tuple:
+        """("loop", channel) of a receive the native executor enqueues."""
+        return ("loop", self.fabric.chan(edge, src, self.rank, lane))
+
+    def check_async(self) -> Optional[str]:
+        return self.fabric.check_async()
+
+    def abort(self) -> None:
+        self.fabric.abort()
+
+    def broadcast_object(self, obj, src: int = 0):
+        return LocalTransport.broadcast_object(self, obj, src)
+
+    def barrier(self) -> None:
+        self.fabric._barrier.wait(timeout=self.fabric.timeout)
+
+
 class LocalTransport(Transport):
     def __init__(self, fabric: LocalFabric, rank: int):
         self.fabric, self.rank, self.world = fabric, rank, fabric.P
@@ -592,6 +819,57 @@ class LocalTransport(Transport):
 
     def barrier(self) -> None:
         self.fabric._barrier.wait(timeout=self.fabric.timeout)
+
+
+class StrictLocalTransport(LocalTransport):
+    """CPU twin of the RCCL data plane's matching rule, for protocol tests.
+
+    One FIFO per (edge, src, dst, lane) -- the communicator layout of
+    `RcclTransport` / `DeviceLoopFabric` -- and every receive checks that
+    the message at its channel's head has the posted size and dtype, raising
+    `TransportError` on a mismatch instead of copying.  `GRAPH_IO` makes the
+    stage worker take its graph-I/O code path (parallel/pipeline.py `_io`):
+    on CPU the decode "graph" body runs eagerly every step, calling
+    `capture_recv` / `capture_send` exactly where a captured graph would.
+    Every op is appended to `fabric.oplog` as (edge, src, dst, lane, dir,
+    bytes, dtype) so tests can compare the two ends of each channel."""
+
+    GRAPH_IO = True
+    SIM_GRAPH_IO = True
+
+    def __init__(self, fabric: LocalFabric, rank: int):
+        super().__init__(fabric, rank)
+        if not hasattr(fabric, "oplog"):
+            fabric.oplog = []  # list.append is atomic under the GIL
+
+    def send(self, t, dst, edge, lane=0):
+        key = ("strict", edge, self.rank, dst, lane)
+        payload = t.detach().clone()
+        self.fabric.oplog.append((edge, self.rank, dst, lane, "send",
+                                  t.numel() * t.element_size(), str(t.dtype)))
+        self.fabric.q(key).put(payload)
+        return SendHandle()
+
+    def _take(self, out, src, edge, lane):
+        key = ("strict", edge, src, self.rank, lane)
+        t = self.fabric.get(key, f"stage {self.rank} waiting on {edge}/lane{lane} from stage {src}")
+        nb, ob = t.numel() * t.element_size(), out.numel() * out.element_size()
+        self.fabric.oplog.append((edge, src, self.rank, lane, "recv", ob, str(out.dtype)))
+        if nb != ob or t.dtype != out.dtype:
+            err = TransportError(f"op order mismatch on {edge} {src}->{self.rank} lane {lane}: posted "
+                                 f"{ob} B {out.dtype}, head message {nb} B {t.dtype}")
+            self.fabric.failed = err
+            raise err
+        out.copy_(t.view(out.shape))
+
+    def irecv(self, out, src, edge, lane=0):
+        return Handle(out, None, post=lambda: self._take(out, src, edge, lane))
+
+    def capture_recv(self, out, src, edge, lane=0):
+        self._take(out, src, edge, lane)  # in stream order: complete on return
+        return Handle(out)
+
+    capture_send = send
 
 
 def init_distributed(backend: str, device_type: str, timeout_s: float = 600.0) -> None:

@@ -60,20 +60,55 @@ class _CaptureGate(racecheck.Shared):
         self._readers = 0
         self._writer = False
         self._waiting = 0
+        self._tls = threading.local()  # this thread's shared-hold depth
 
-    @contextlib.contextmanager
-    def shared(self):
+    def _depth(self) -> int:
+        return getattr(self._tls, "depth", 0)
+
+    def _acquire_shared(self) -> None:
         with self._cv:
             while self._writer or self._waiting:
                 self._cv.wait()
             self._readers += 1
+
+    def _release_shared(self) -> None:
+        with self._cv:
+            self._readers -= 1
+            if self._readers == 0:
+                self._cv.notify_all()
+
+    @contextlib.contextmanager
+    def shared(self):
+        """Shared hold; re-entrant per thread (a nested hold never waits, so
+        a thread inside a GPU section cannot block behind a waiting capture
+        that waits for it)."""
+        d = self._depth()
+        if d == 0:
+            self._acquire_shared()
+        self._tls.depth = d + 1
         try:
             yield
         finally:
-            with self._cv:
-                self._readers -= 1
-                if self._readers == 0:
-                    self._cv.notify_all()
+            self._tls.depth = d
+            if d == 0:
+                self._release_shared()
+
+    @contextlib.contextmanager
+    def released(self):
+        """Drop this thread's shared hold (if any) around a blocking wait --
+        a transport handshake, an exclusive capture -- and take it back
+        after."""
+        d = self._depth()
+        if d == 0:
+            yield
+            return
+        self._tls.depth = 0
+        self._release_shared()
+        try:
+            yield
+        finally:
+            self._acquire_shared()
+            self._tls.depth = d
 
     @contextlib.contextmanager
     def exclusive(self):
@@ -155,6 +190,8 @@ class GroupState(racecheck.Shared):
             self.hd = torch.empty(cap, H, dtype=torch.float32, device=dev)  # decode hidden in/out
         self.hp: Optional[torch.Tensor] = None  # prefill hidden receive buffer (grown)
         self.graphs: Dict[tuple, tuple] = {}
+        # loopback graph I/O: key -> (native I/O-list handle, [(chan, dir, bytes)])
+        self.graph_io: Dict[tuple, tuple] = {}
         self.seen: set = set()
         self._metas: Dict[tuple, BatchMeta] = {}
         self.rows_n = 0
@@ -181,6 +218,14 @@ class GroupState(racecheck.Shared):
             self.tokret = new
         if w.first:
             self.tin = new
+        self.drop_graphs(w)
+
+    def drop_graphs(self, w: "StageWorker") -> None:
+        free = getattr(w.t, "C", None)
+        for io, _ in self.graph_io.values():
+            if io and free is not None:
+                free.loop_io_free(io)
+        self.graph_io.clear()
         self.graphs.clear()
         self.seen.clear()
 
@@ -268,6 +313,9 @@ class StageWorker(racecheck.Shared):
         # bound ones (attention over the KV cache).  Each lane has its own
         # split-K ticket counters in the backend.
         n_lanes = int(os.environ.get("LSD_LANES", "2"))
+        # lane index of a group, also on CPU (no streams there): transports
+        # keep one channel per (edge, lane), as the RCCL communicators do
+        self.n_lanes = max(1, n_lanes)
         self.lanes = ([torch.cuda.Stream(self.device) for _ in range(n_lanes)]
                       if self.device.type == "cuda" else [])
         # LSD_LANE_CU_MASK: give each lane its own share of the CUs (spatial
@@ -288,14 +336,16 @@ class StageWorker(racecheck.Shared):
         self.readout = None        # stage 0: callable(step, plan, ret_tensor) for token readout
         # stage 0, native executor: callable(plan, gp, pinned host ids, event, release)
         self.readout_native = None
-        self._tls = threading.local()
         # Decode graphs that contain their own edge receive and send (native
-        # RCCL transport, parallel/comm.py RcclTransport): a decode item is
-        # then ONE graph launch per stage.  Items carrying prefill chunks keep
-        # eager transfers (their sizes vary), as does stage 0's token-return
-        # receive (the host reads it back and may re-gather the rows).
+        # RCCL transport, parallel/comm.py RcclTransport, or its single-GPU
+        # rehearsal DeviceLoopTransport): a decode item is then ONE graph
+        # launch per stage.  Items carrying prefill chunks keep eager
+        # transfers (their sizes vary), as does stage 0's token-return
+        # receive (the host reads it back and may re-gather the rows).  On
+        # CPU, StrictLocalTransport runs the same code path with the graph
+        # body executed eagerly (protocol tests).
         self.graph_io = bool(transport is not None and getattr(transport, "GRAPH_IO", False)
-                             and self.device.type == "cuda"
+                             and (self.device.type == "cuda" or getattr(transport, "SIM_GRAPH_IO", False))
                              and os.environ.get("LSD_GRAPH_IO", "1") != "0")
         # Native stage executor (csrc/stage_exec.cpp): a step made only of
         # steady-state decode items is enqueued by one C++ call (see
@@ -307,6 +357,7 @@ class StageWorker(racecheck.Shared):
         self._tev_free: List[torch.cuda.Event] = []  # busy-timing events
         self._tev_used: List[torch.cuda.Event] = []
         self.native_steps = 0
+        self.io_items = 0  # decode items whose (graph) body carried its own transfers
 
     # ------------------------------------------------------------------
     def configure(self, groups: int, cap: int) -> None:
@@ -318,7 +369,7 @@ class StageWorker(racecheck.Shared):
         self.recv.clear()
 
     def lane_of(self, g: int) -> int:
-        return g % max(1, len(self.lanes))
+        return g % self.n_lanes
 
     def _io(self, gp: GroupPlan) -> bool:
         """Does this item's decode graph carry its own receive / send?"""
@@ -407,13 +458,29 @@ class StageWorker(racecheck.Shared):
                 self._item(plan, gp, nx)
 
     def _new_event(self, timing: bool) -> torch.cuda.Event:
-        """A created (recorded once) event whose raw handle C++ can record."""
+        """A created (recorded once) event whose raw handle C++ can record
+        (call inside the gate: the first record is a stream operation)."""
         pool = self._tev_free if timing else self._ev_free
         if pool:
             return pool.pop()
         ev = torch.cuda.Event(enable_timing=timing)
         ev.record(self.lanes[0])
         return ev
+
+    def _pinned(self, gs: GroupState, n: int) -> torch.Tensor:
+        """Pinned host buffer for one token readout of group gs: a ring per
+        group (a slot is reused only after `lag` more readouts of the group,
+        long after the scheduler applied it -- Engine._drive blocks on
+        readouts older than P + 2 steps)."""
+        ring = getattr(gs, "_pin_ring", None)
+        if ring is None or ring.shape[1] < n:
+            ring = torch.empty(self._PIN_SLOTS, max(n, gs.cap), dtype=torch.int32, pin_memory=True)
+            gs._pin_ring, gs._pin_next = ring, 0
+        k = gs._pin_next
+        gs._pin_next = (k + 1) % self._PIN_SLOTS
+        return ring[k, :n]
+
+    _PIN_SLOTS = 64
 
     def _native_step(self, plan: StepPlan, items: List[GroupPlan]) -> bool:
         """Enqueue this step with one C++ call (csrc/stage_exec.cpp exec_items)
@@ -431,37 +498,72 @@ class StageWorker(racecheck.Shared):
             if self.P > 1 and not io:
                 return False
             gs = self.groups[gp.g]
-            ent = gs.graphs.get((gp.b, gp.ctxb, io))
+            key = (gp.b, gp.ctxb, io)
+            ent = gs.graphs.get(key)
             if ent is None:
                 return False
             ret = gp.ret if self.first else 0
             if ret and (gs.tin.numel() < ret or (self.readout is not None and self.readout_native is None)):
                 return False
-            descs.append((gp, gs, ent[0], ret))
+            descs.append((gp, gs, ent[0], ret, gs.graph_io.get(key)))
+        if getattr(self.t, "aborted", False):
+            from .comm import TransportError
+
+            raise TransportError("data plane aborted: step not issued")
         timing = plan.timing and self.stats is not None
         C = self.stage.backend.C
+        nf = C.exec_fields()
+        # loopback channels: the step's whole op sequence passes the enqueue
+        # handshake here, outside the gate; exec_items' own checks are then
+        # instant (csrc/loop_fabric.cpp)
+        pre: List[tuple] = []
         rows, reads = [], []
-        for gp, gs, g, ret in descs:
-            lane = self.lanes[self.lane_of(gp.g)]
-            d = [0] * 12
-            d[0] = g.raw_cuda_graph_exec()
-            d[1] = lane.cuda_stream
+        recv_kind = []
+        for gp, gs, g, ret, gio in descs:
+            rk = None
             if ret and self.P > 1:  # token-return receive from the last stage
-                h, me = self.t._edge("ret", self.P - 1, self.r, self.lane_of(gp.g))
-                d[2], d[3], d[4], d[5] = h, gs.tin.data_ptr(), 4 * ret, 1 - me
-            if timing:
-                t0, t1 = self._new_event(True), self._new_event(True)
-                self._tev_used += (t0, t1)
-                self.stats.marks.append((t0, t1))
-                d[6], d[11] = t0.cuda_event, t1.cuda_event
-            if ret and self.readout is not None:
-                host = torch.empty(ret, dtype=torch.int32, pin_memory=True)
-                ev = self._new_event(False)
-                d[7], d[8], d[9], d[10] = gs.tin.data_ptr(), host.data_ptr(), 4 * ret, ev.cuda_event
-                reads.append((gp, host, ev))
-            rows.append(d)
+                rk = self.t.native_recv("ret", self.P - 1, self.lane_of(gp.g))
+                if rk[0] == "loop":
+                    pre.append((rk[1], 1, 4 * ret))
+            if gio is not None:
+                pre.extend(gio[1])
+            recv_kind.append(rk)
+        if pre:
+            self.t.prewait(pre)
         with self._gpu():
-            C.exec_items(rows)
+            for (gp, gs, g, ret, gio), rk in zip(descs, recv_kind):
+                lane = self.lanes[self.lane_of(gp.g)]
+                d = [0] * nf
+                d[0] = g.raw_cuda_graph_exec()
+                d[1] = lane.cuda_stream
+                if rk is not None:
+                    if rk[0] == "rccl":
+                        d[2], d[5] = rk[1], rk[2]
+                    else:
+                        d[12] = rk[1]
+                    d[3], d[4] = gs.tin.data_ptr(), 4 * ret
+                if gio is not None:
+                    d[13] = gio[0]
+                if timing:
+                    t0, t1 = self._new_event(True), self._new_event(True)
+                    self._tev_used += (t0, t1)
+                    self.stats.marks.append((t0, t1))
+                    d[6], d[11] = t0.cuda_event, t1.cuda_event
+                if ret and self.readout is not None:
+                    host = self._pinned(gs, ret)
+                    ev = self._new_event(False)
+                    d[7], d[8], d[9], d[10] = gs.tin.data_ptr(), host.data_ptr(), 4 * ret, ev.cuda_event
+                    reads.append((gp, host, ev))
+                rows.append(d)
+            try:
+                with (self.t.issuing() if self.t is not None else contextlib.nullcontext()):
+                    C.exec_items(rows)
+            except RuntimeError:
+                # copies of the items already enqueued may still target the
+                # pinned buffers: let them land before the buffers can be reused
+                for lane in self.lanes:
+                    lane.synchronize()
+                raise
         for gp, host, ev in reads:
             self.readout_native(plan, gp, host, ev, self._ev_free.append)
         self.native_steps += 1
@@ -614,6 +716,8 @@ class StageWorker(racecheck.Shared):
         # I/O the graph receives its input and sends its output itself
         io = self._io(gp)
         lane = self.lane_of(gp.g)
+        if io:
+            self.io_items += 1
         if gp.b > 0:
             inp = gs.tin[: gp.b] if self.first else (gs.hd[: gp.b] if io else ins[k])
             out = self._decode(gp, gs, inp, io)
@@ -709,16 +813,34 @@ class StageWorker(racecheck.Shared):
             return body()
         if key in gs.graphs:
             g, out = gs.graphs[key]
-            g.replay()  # inside the item's shared section of GPU_GATE
+            self._replay(gs, key, g)  # inside the item's shared section of GPU_GATE
             return out
         if key not in gs.seen:  # first use: eager (allocates workspaces outside capture)
             gs.seen.add(key)
             return body()
-        gs.graphs[key] = self._capture(body)
+        g, out, io = self._capture(body)
+        gs.graphs[key] = (g, out)
+        if io[0]:
+            gs.graph_io[key] = io
         self.captures += 1
-        g, out = gs.graphs[key]
-        g.replay()
+        self._replay(gs, key, g)
         return out
+
+    def _replay(self, gs: GroupState, key: tuple, g) -> None:
+        if getattr(self.t, "aborted", False):
+            # never replay a graph whose captured transfers use an aborted
+            # data plane (freed communicators / abandoned channels)
+            from .comm import TransportError
+
+            raise TransportError("data plane aborted: decode graph not replayed")
+        io = gs.graph_io.get(key)
+        if io is not None:
+            self.t.replay(g, io[0], io[1])  # loopback: enqueue handshake around the launch
+        elif key[2]:
+            with self.t.issuing():  # captured RCCL ops: not beside an abort
+                g.replay()
+        else:
+            g.replay()
 
     def _fwd_b(self, gp: GroupPlan, ins) -> None:
         """Compat /forward_b on stages 1..P-1: full-sequence forward of the
@@ -747,6 +869,8 @@ class StageWorker(racecheck.Shared):
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
+        begin = getattr(self.t, "begin_capture", None)
+        io = (0, [])
         with self._gate_released(), GPU_GATE.exclusive():
             # no garbage collection inside the capture: a collected object
             # from an earlier session (a graph, an event, a communicator)
@@ -756,47 +880,31 @@ class StageWorker(racecheck.Shared):
             gc.disable()
             try:
                 with torch.cuda.stream(s):
+                    if begin is not None:
+                        begin()  # the transport records the ops captured below
                     g.capture_begin(capture_error_mode="thread_local")
                     try:
                         out = fn()
                     finally:
                         g.capture_end()
+                        if begin is not None:
+                            io = self.t.end_capture()
             finally:
                 if was:
                     gc.enable()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        return g, out
+        return g, out, io
 
-    @contextlib.contextmanager
     def _gate_released(self):
         """Drop this thread's shared hold on GPU_GATE (held by the item being
         executed) around an exclusive section, and take it back after."""
-        held = getattr(self._tls, "shared", None)
-        if held is None:
-            yield
-            return
-        held.__exit__(None, None, None)
-        try:
-            yield
-        finally:
-            cm = GPU_GATE.shared()
-            cm.__enter__()
-            self._tls.shared = cm
+        return GPU_GATE.released()
 
-    @contextlib.contextmanager
     def _gpu(self):
         """Shared hold on GPU_GATE for a GPU-issuing section of this thread."""
         if self.device.type != "cuda":
-            yield
-            return
-        cm = GPU_GATE.shared()
-        cm.__enter__()
-        self._tls.shared = cm
-        try:
-            yield
-        finally:
-            self._tls.shared.__exit__(None, None, None)
-            self._tls.shared = None
+            return contextlib.nullcontext()
+        return GPU_GATE.shared()
 
 
 def _cu_masked_lanes(dev: torch.device, n: int, mode: str) -> List[torch.cuda.ExternalStream]:

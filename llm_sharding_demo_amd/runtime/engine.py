@@ -39,8 +39,8 @@ import torch
 from ..config import EngineConfig, SamplingParams
 from ..utils import racecheck
 from ..models.stage import StageModel
-from ..parallel.comm import (GlooPlanChannel, LocalFabric, LocalPlanChannel, Transport,
-                             TransportError, init_distributed, make_dist_transport)
+from ..parallel.comm import (DeviceLoopFabric, GlooPlanChannel, LocalFabric, LocalPlanChannel,
+                             Transport, TransportError, init_distributed, make_dist_transport)
 from ..parallel.partition import make_alt_unit_plans, make_unit_plan, union_plan, units_to_layers
 from ..parallel.pipeline import StageWorker
 from .kv_cache import KVCache, SlotAllocator, plan_slots
@@ -125,12 +125,23 @@ class Engine(racecheck.Shared):
                 dev = resolve_device(cfg.device)
                 devices = [str(dev)] * self.P
             self.devices = [_with_index(torch.device(d)) for d in devices]
+            on_gpu = self.devices[0].type == "cuda"
+            # "devloop": device loopback channels with graph I/O and the native
+            # executor at P > 1 -- the single-GPU rehearsal of the RCCL data
+            # plane (parallel/comm.py DeviceLoopFabric), allocated before the
+            # KV cache sizes itself from free HBM.  "loopback": device-async
+            # event hand-off between stage threads.  "strict": host queues per
+            # (edge, lane) with receive-size checks and the graph-I/O code path
+            # (CPU protocol tests).  Else plain host queues.
+            kind = {"loopback": "loopback" if on_gpu else "local",
+                    "devloop": "devloop" if on_gpu else "strict",
+                    "strict": "strict"}.get(cfg.transport, "local")
+            self.fabric = None
+            if self.P > 1:
+                self.fabric = (self._devloop_fabric(self.devices[0]) if kind == "devloop"
+                               else LocalFabric(self.P, fault=fault))
             self.kv_slots = self._kv_slots(self.devices)
             self.stages = [self._build_stage(i, self.devices[i]) for i in range(self.P)]
-            self.fabric = LocalFabric(self.P, fault=fault) if self.P > 1 else None
-            # "loopback": device-async event hand-off between stage threads on
-            # GPUs (single-GPU rehearsal of the RCCL schedule); else host queues
-            kind = "loopback" if (cfg.transport == "loopback" and self.devices[0].type == "cuda") else "local"
             self.workers = [self._worker(st, self.fabric.transport(i, kind) if self.fabric else None, i)
                             for i, st in enumerate(self.stages)]
             self.rank = 0
@@ -177,9 +188,12 @@ class Engine(racecheck.Shared):
         else:
             raise ValueError(f"unknown mode {mode!r}")
         # dist mode: every rank watches its own progress and data plane (a
-        # follower stuck behind a dead peer aborts its communicators too)
+        # follower stuck behind a dead peer aborts its communicators too);
+        # the device-loopback rehearsal has a data plane to abort as well
+        self.data_plane = self.transport if mode == "dist" else (
+            self.fabric if isinstance(self.fabric, DeviceLoopFabric) else None)
         self.watchdog = None
-        if mode == "dist" and cfg.round_timeout_s > 0:
+        if self.data_plane is not None and cfg.round_timeout_s > 0:
             from .scheduler import Watchdog
 
             self.watchdog = Watchdog(self, cfg.round_timeout_s)
@@ -189,7 +203,6 @@ class Engine(racecheck.Shared):
         self.scheduler = Scheduler(self, self.M, self.group_cap)
         if self.rank == 0:
             self.workers[0].readout = self.scheduler.on_readout
-            self.workers[0].readout_native = self.scheduler.on_readout_native
             self.workers[0].readout_native = self.scheduler.on_readout_native
         for w in self.workers:
             w.use_graphs = cfg.use_graphs
@@ -238,6 +251,18 @@ class Engine(racecheck.Shared):
         if fits < want:
             log.warning("KV budget: %d of %d requested slots fit", fits, want)
         return fits
+
+    def _devloop_fabric(self, dev: torch.device) -> DeviceLoopFabric:
+        """Loopback channels sized for the largest message an edge carries:
+        one item's prefill rows (a group's chunk tokens, fp32) or decode rows;
+        two of them fit each ring.  LSD_LOOP_RING_MB overrides."""
+        cfg, H = self.cfg, self.mcfg.hidden
+        per_seq = cfg.prefill_chunk if cfg.prefill_chunk > 0 else self.max_seq
+        big = self.group_cap * min(per_seq, self.max_seq) * H * 4
+        ring = int(os.environ.get("LSD_LOOP_RING_MB", "0")) << 20 or max(8 << 20, 2 * big + (1 << 20))
+        return DeviceLoopFabric(self.P, dev, lanes=int(os.environ.get("LSD_LANES", "2")), ring_bytes=ring,
+                                timeout=cfg.round_timeout_s,
+                                spin_limit_s=float(os.environ.get("LSD_LOOP_SPIN_S", "30")))
 
     def _weight_bytes(self, i: int) -> int:
         mc = self.mcfg

@@ -703,7 +703,7 @@ class Watchdog:
         while not self._stop.wait(self.poll):
             if self.fired:
                 continue
-            tr = getattr(self.engine, "transport", None)
+            tr = getattr(self.engine, "data_plane", None) or getattr(self.engine, "transport", None)
             try:
                 err = tr.check_async() if tr is not None else None
             except Exception as e:  # noqa: BLE001 - a broken communicator is an error too
@@ -724,7 +724,7 @@ class Watchdog:
         log.error("watchdog: %s: %s; marking engine unhealthy and aborting the data plane", kind, msg)
         self.engine.healthy = False
         self.engine.last_error = f"{kind}: {msg}"
-        tr = getattr(self.engine, "transport", None)
+        tr = getattr(self.engine, "data_plane", None) or getattr(self.engine, "transport", None)
         if tr is not None:
             try:
                 tr.abort()
