@@ -121,7 +121,7 @@ class _DistTransport(Transport):
 
     EDGE_GROUPS = True  # a torch process group per pipeline edge
 
-    def __init__(self, num_stages: int, replicas: int = 1):
+    def __init__(self, num_stages: int, replicas: int = 1, timeout_s: Optional[float] = None):
         import torch.distributed as dist
 
         self.dist = dist
@@ -133,17 +133,21 @@ class _DistTransport(Transport):
         self.P, self.R = P, R
         self.replica, self.rank = divmod(self.grank, P)  # rank = stage index
         self.world = P
-        # Groups must be created by every rank in the same order.
+        # Groups must be created by every rank in the same order.  Edge and
+        # control groups get the engine's round deadline (new_group does not
+        # inherit the default group's timeout: gloo would wait 30 min on a
+        # dead peer)
+        kw = {"timeout": datetime.timedelta(seconds=timeout_s)} if timeout_s else {}
         self.groups: Dict[str, object] = {}
         for rep in range(R):
             base = rep * P
             for i in range(P - 1):
-                self.groups[f"r{rep}fwd{i}"] = (dist.new_group([base + i, base + i + 1], backend=self._backend())
-                                                if self.EDGE_GROUPS else None)
+                self.groups[f"r{rep}fwd{i}"] = (dist.new_group([base + i, base + i + 1], backend=self._backend(),
+                                                               **kw) if self.EDGE_GROUPS else None)
             if P > 1:
-                self.groups[f"r{rep}ret"] = (dist.new_group([base + P - 1, base], backend=self._backend())
+                self.groups[f"r{rep}ret"] = (dist.new_group([base + P - 1, base], backend=self._backend(), **kw)
                                              if self.EDGE_GROUPS else None)
-        self.ctrl = dist.new_group(list(range(P * R)), backend="gloo")
+        self.ctrl = dist.new_group(list(range(P * R)), backend="gloo", **kw)
         # step plans (rank 0 -> every rank) and DP token readouts (replica
         # stage 0 -> rank 0) travel on their own gloo groups with no practical
         # timeout: an idle server waits on them indefinitely
@@ -303,8 +307,9 @@ class RcclTransport(_DistTransport):
     def _backend(self) -> str:
         return "gloo"  # control plane only; the data plane is native
 
-    def __init__(self, num_stages: int, replicas: int = 1, lanes: int = 2):
-        super().__init__(num_stages, replicas)
+    def __init__(self, num_stages: int, replicas: int = 1, lanes: int = 2,
+                 timeout_s: Optional[float] = None):
+        super().__init__(num_stages, replicas, timeout_s)
         from ..ops.hip import _load
 
         self.C = _load()
@@ -898,19 +903,21 @@ def init_distributed(backend: str, device_type: str, timeout_s: float = 600.0) -
     dist.init_process_group(backend=backend, **kw)
 
 
-def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1) -> Transport:
+def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1,
+                        timeout_s: Optional[float] = None) -> Transport:
     if kind == "rccl":  # native communicator (csrc/comm.cpp), one per (edge, lane)
         import os
 
-        t = RcclTransport(num_stages, replicas, lanes=int(os.environ.get("LSD_LANES", "2")))
+        t = RcclTransport(num_stages, replicas, lanes=int(os.environ.get("LSD_LANES", "2")),
+                          timeout_s=timeout_s)
         t.warmup(device)
         return t
     if kind == "nccl":
-        t = NcclTransport(num_stages, replicas)
+        t = NcclTransport(num_stages, replicas, timeout_s)
         t.warmup(device)
         return t
     if kind == "gloo":
-        t = GlooTransport(num_stages, replicas)
+        t = GlooTransport(num_stages, replicas, timeout_s)
         t.warmup(device)  # same edge-by-edge bring-up as RCCL (host tensors)
         return t
     raise ValueError(f"unknown transport {kind!r}")

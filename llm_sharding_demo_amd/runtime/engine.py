@@ -119,6 +119,7 @@ class Engine(racecheck.Shared):
         # LSD_HOST_PROFILE=1: host seconds in (plan, issue, readout wait), steps
         self._hostprof = [0.0, 0.0, 0.0, 0, 0, 0.0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
         self.kv_slots = 0
+        self._stall_after: Optional[int] = None  # test hook, see _test_stall
 
         if mode == "local":
             if devices is None:
@@ -164,8 +165,10 @@ class Engine(racecheck.Shared):
             if dev.type == "cuda":
                 dev = torch.device("cuda", torch.cuda.current_device())
             self.devices = [dev]
-            self.transport = make_dist_transport(self.P, kind, dev, self.R)
+            self.transport = make_dist_transport(self.P, kind, dev, self.R, cfg.round_timeout_s)
             self.replica, self.stage_idx = self.transport.replica, self.transport.rank
+            if os.environ.get("LSD_TEST_STALL_RANK") == str(self.rank):
+                self._stall_after = int(os.environ.get("LSD_TEST_STALL_AFTER", "0"))
             self.kv_slots = self._kv_slots([dev], collective=True)
             stage = self._build_stage(self.stage_idx, dev)
             self.stages = [stage]
@@ -502,11 +505,25 @@ class Engine(racecheck.Shared):
                 started = True
             nxt = recv()
             self._round(time.monotonic())  # watchdog: host blocked inside a step
+            if self._stall_after is not None:
+                self._test_stall()
             worker.run_step(cur, nxt if not nxt.stop else None)
             self._round(None)
             if not self.healthy:
                 raise RuntimeError(self.last_error)
             cur = nxt
+
+    def _test_stall(self) -> None:
+        """Test hook (LSD_TEST_STALL_RANK / LSD_TEST_STALL_AFTER): this rank
+        stops issuing work after that many steps, as a hung peer process
+        would; it waits for its own watchdog, then fails."""
+        self._stall_after -= 1
+        if self._stall_after >= 0:
+            return
+        log.error("test hook: rank %d stalls", self.rank)
+        while self.healthy:
+            time.sleep(0.05)
+        raise RuntimeError("test stall")
 
     def _follower_stats(self, worker: StageWorker, end_plan: StepPlan) -> None:
         if not end_plan.timing:
