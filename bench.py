@@ -223,7 +223,8 @@ def main() -> int:
         print(json.dumps(out), flush=True)
         hp = getattr(eng, "_hostprof", None)
         if hp is not None and hp[3]:
-            print(f"host per decode step: plan {hp[0] / hp[3] * 1e6:.1f} us, issue {hp[1] / hp[3] * 1e6:.1f} us "
+            print(f"host per decode step: plan {hp[0] / hp[3] * 1e6:.1f} us (of which plan send "
+              f"{hp[6] / hp[3] * 1e6:.1f} us, {hp[7] / hp[3]:.0f} B), issue {hp[1] / hp[3] * 1e6:.1f} us "
                   f"({hp[1] / max(hp[4], 1) * 1e6:.1f} us per item; issuing-thread CPU "
                   f"{hp[5] / max(hp[4], 1) * 1e6:.1f} us per item), readout wait "
                   f"{hp[2] / hp[3] * 1e6:.1f} us over {hp[3]} steps", file=sys.stderr)

@@ -202,6 +202,10 @@ class SchedCore {
   };
   struct Group {
     std::vector<int64_t> rows, prefilling;
+    // rows' Seq entries (node-based map: stable until a sequence is erased,
+    // which happens only after it left its group), so the steady-state step
+    // touches each row through a pointer instead of three hash lookups
+    std::vector<Seq*> rowp;
     int64_t prev = -1;  // produced_ id of the last token-producing item
   };
 
@@ -246,19 +250,37 @@ class SchedCore {
       ret = prev->b + (int)prev->finals.size();
     }
     // leaves: every token scheduled, or EOS read back
-    std::vector<int64_t> keep;
-    for (int64_t sid : gh.rows) {
-      const Seq& s = seqs_.at(sid);
-      if (s.issued >= s.want || s.stop) {
-        ++leaves_;
-        if (prev) prev->release.push_back(sid);
-      } else {
-        keep.push_back(sid);
+    bool any_leave = false;
+    for (const Seq* s : gh.rowp)
+      if (s->issued >= s->want || s->stop) {
+        any_leave = true;
+        break;
       }
+    // steady state (no leave, no newly sampled prefill): the rows stay put
+    const bool same = !any_leave && !(prev && !prev->finals.empty());
+    std::vector<int64_t> new_rows;
+    std::vector<Seq*> new_p;
+    if (same) {
+      new_rows = gh.rows;
+    } else {
+      for (size_t i = 0; i < gh.rows.size(); ++i) {
+        const int64_t sid = gh.rows[i];
+        Seq* s = gh.rowp[i];
+        if (s->issued >= s->want || s->stop) {
+          ++leaves_;
+          if (prev) prev->release.push_back(sid);
+        } else {
+          new_rows.push_back(sid);
+          new_p.push_back(s);
+        }
+      }
+      if (prev)
+        for (int64_t sid : prev->finals) {
+          new_rows.push_back(sid);
+          new_p.push_back(&seqs_.at(sid));
+        }
     }
-    std::vector<int64_t> new_rows = keep;
-    if (prev) new_rows.insert(new_rows.end(), prev->finals.begin(), prev->finals.end());
-    changed = new_rows != gh.rows;
+    changed = !same && new_rows != gh.rows;
     // joins (capacity counts rows + sequences still prefilling)
     const int room = cap_ - (int)new_rows.size() - (int)gh.prefilling.size();
     for (int64_t sid : admit(rep, g, room, admitted)) gh.prefilling.push_back(sid);
@@ -287,11 +309,13 @@ class SchedCore {
     // decode rows
     n = (int)new_rows.size();
     b = bucket(n, cap_);
+    const std::vector<Seq*>& rp = same ? gh.rowp : new_p;
     if (changed) {
       std::unordered_map<int64_t, int> old_index;
       for (size_t i = 0; i < gh.rows.size(); ++i) old_index[gh.rows[i]] = (int)i;
-      for (int64_t sid : new_rows) {
-        const Seq& s = seqs_.at(sid);
+      for (size_t k = 0; k < new_rows.size(); ++k) {
+        const int64_t sid = new_rows[k];
+        const Seq& s = *rp[k];
         int src;
         auto f = old_index.find(sid);
         if (f != old_index.end()) {
@@ -305,17 +329,19 @@ class SchedCore {
     }
     if (n) {
       int top = 0;
-      for (int64_t sid : new_rows) top = std::max(top, seqs_.at(sid).pos);
+      for (const Seq* s : rp) top = std::max(top, s->pos);
       top += 1;
       ctxb = std::min((top + 255) / 256 * 256, max_seq_);
-      for (int64_t sid : new_rows) {  // one token per decode row this step
-        Seq& s = seqs_.at(sid);
-        s.issued += 1;
-        s.pos += 1;
-        s.sstep += 1;
+      for (Seq* s : rp) {  // one token per decode row this step
+        s->issued += 1;
+        s->pos += 1;
+        s->sstep += 1;
       }
     }
-    gh.rows = new_rows;
+    if (!same) {
+      gh.rows = new_rows;
+      gh.rowp = std::move(new_p);
+    }
     max_rows_ = std::max(max_rows_, n);
     if (b || !finals.empty()) {
       Produced np;

@@ -31,6 +31,7 @@ owes on an earlier item.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import datetime
 import pickle
@@ -463,28 +464,72 @@ class LocalPlanChannel:
 
 
 class GlooPlanChannel:
-    """torch.distributed gloo p2p on a dedicated group: an object is pickled
-    (our own plan / token records, produced by this job's ranks) and sent as
-    a size message + a byte payload.  Sends are non-blocking (isend), so the
-    scheduler never waits on a slow follower; each receiver posts blocking
-    receives from its single source in FIFO order."""
+    """torch.distributed gloo p2p on a dedicated group.  Step plans use the
+    binary record of runtime/plan.py (one fixed-size int32 message per plan in
+    steady-state decode; a pickled plan -- our own records, produced by this
+    job's rank 0 -- only follows on composition changes, prefill chunks and
+    compat forwards).  Other objects (token readouts of DP replicas) are
+    pickled as a size message + a byte payload.  Sends are non-blocking
+    (isend), so the scheduler never waits on a slow follower; each receiver
+    posts blocking receives from its single source in FIFO order.
+    `plans=False` selects the plain pickled-object channel."""
 
-    def __init__(self, group, tag: int = 1):
+    def __init__(self, group, tag: int = 1, plans: bool = True):
         import torch.distributed as dist
 
         self.dist, self.pg, self.tag = dist, group, tag
-        self._works: List[tuple] = []
+        self.plans = plans
+        # posted sends, oldest first; completed ones are dropped from the
+        # front (a scan of the whole list per send cost ~2 ms per step at
+        # 7 followers x 64 steps of look-ahead: profiles/r4_plan_wire.log)
+        self._works: "collections.deque" = collections.deque()
+        self._enc: Dict[int, object] = {}
+        self._dec: Dict[int, object] = {}
+        self.bytes_sent = 0
+        self.msgs_sent = 0
+
+    def _isend(self, t: torch.Tensor, dst: int, tag: int):
+        self.bytes_sent += t.numel() * t.element_size()
+        self.msgs_sent += 1
+        return self.dist.isend(t, dst, group=self.pg, tag=tag)
 
     def send(self, dst: int, obj) -> None:
-        data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
-        n = torch.tensor([len(data)], dtype=torch.int64)
-        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8)
-        w1 = self.dist.isend(n, dst, group=self.pg, tag=self.tag)
-        w2 = self.dist.isend(buf, dst, group=self.pg, tag=self.tag + 1)
-        self._works.append((w1, w2, n, buf))
-        self._works = [w for w in self._works if not (w[0].is_completed() and w[1].is_completed())]
+        if self.plans:
+            from ..runtime.plan import PlanEncoder
+
+            enc = self._enc.get(dst)
+            if enc is None:
+                enc = self._enc[dst] = PlanEncoder()
+            rec, payload = enc.encode(obj)
+            hdr = torch.from_numpy(rec)
+            works = [self._isend(hdr, dst, self.tag), hdr]
+            if payload is not None:
+                buf = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+                works += [self._isend(buf, dst, self.tag + 1), buf]
+        else:
+            data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+            n = torch.tensor([len(data)], dtype=torch.int64)
+            buf = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            works = [self._isend(n, dst, self.tag), n, self._isend(buf, dst, self.tag + 1), buf]
+        self._works.append(tuple(works))
+        while self._works and all(x.is_completed() for x in self._works[0][0::2]):
+            self._works.popleft()
 
     def recv(self, src: int):
+        if self.plans:
+            from ..runtime.plan import PLAN_WORDS, PlanDecoder
+
+            dec = self._dec.get(src)
+            if dec is None:
+                dec = self._dec[src] = PlanDecoder()
+            hdr = torch.empty(PLAN_WORDS, dtype=torch.int32)
+            self.dist.recv(hdr, src, group=self.pg, tag=self.tag)
+
+            def payload(nbytes: int) -> bytes:
+                buf = torch.empty(nbytes, dtype=torch.uint8)
+                self.dist.recv(buf, src, group=self.pg, tag=self.tag + 1)
+                return buf.numpy().tobytes()
+            return dec.decode(hdr.numpy(), payload)
         n = torch.empty(1, dtype=torch.int64)
         self.dist.recv(n, src, group=self.pg, tag=self.tag)
         buf = torch.empty(int(n[0]), dtype=torch.uint8)
@@ -492,9 +537,9 @@ class GlooPlanChannel:
         return pickle.loads(buf.numpy().tobytes())
 
     def flush(self) -> None:
-        for w1, w2, _, _ in self._works:
-            w1.wait()
-            w2.wait()
+        for w in self._works:
+            for x in w[0::2]:
+                x.wait()
         self._works.clear()
 
 

@@ -116,8 +116,9 @@ class Engine(racecheck.Shared):
         self.loop_thread: Optional[threading.Thread] = None
         self._stop_loop = threading.Event()
         self._wake = threading.Event()  # a request was submitted (serving loop)
-        # LSD_HOST_PROFILE=1: host seconds in (plan, issue, readout wait), steps
-        self._hostprof = [0.0, 0.0, 0.0, 0, 0, 0.0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
+        # LSD_HOST_PROFILE=1: host seconds in (plan, issue, readout wait), steps,
+        # items, issuing-thread CPU, plan-send seconds, plan bytes sent
+        self._hostprof = [0.0, 0.0, 0.0, 0, 0, 0.0, 0.0, 0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
         self.kv_slots = 0
         self._stall_after: Optional[int] = None  # test hook, see _test_stall
 
@@ -174,8 +175,10 @@ class Engine(racecheck.Shared):
             self.stages = [stage]
             self.workers = [self._worker(stage, self.transport, self.stage_idx)]
             self.fabric = None
-            self.plan_ch = GlooPlanChannel(self.transport.plan_pg, tag=1)
-            self.tok_ch = GlooPlanChannel(self.transport.tok_pg, tag=3)
+            # LSD_PLAN_WIRE=pickle: the pre-binary control plane (A/B only)
+            self.plan_ch = GlooPlanChannel(self.transport.plan_pg, tag=1,
+                                           plans=os.environ.get("LSD_PLAN_WIRE", "binary") != "pickle")
+            self.tok_ch = GlooPlanChannel(self.transport.tok_pg, tag=3, plans=False)
             self._tok_threads: List[threading.Thread] = []
             if self.rank == 0:
                 for rep in range(1, self.R):
@@ -408,6 +411,8 @@ class Engine(racecheck.Shared):
                 t0 = time.monotonic()
                 self._round(t0)
                 nxt = sch.build_step()
+                tb = time.monotonic()
+                b0 = getattr(self.plan_ch, "bytes_sent", 0)
                 self._send_plans(nxt)
                 t1 = time.monotonic()
                 c1 = time.thread_time() if hp is not None else 0.0
@@ -423,6 +428,8 @@ class Engine(racecheck.Shared):
                     hp[3] += 1
                     hp[4] += sum(1 for gp in cur[0].groups if gp.has_work)
                     hp[5] += c2 - c1  # CPU time of the issuing thread (no waits)
+                    hp[6] += t1 - tb  # encoding + posting the followers' plans
+                    hp[7] += getattr(self.plan_ch, "bytes_sent", 0) - b0
                 cur = nxt
             if ran:
                 w0.end_session()

@@ -99,3 +99,99 @@ class StepPlan:
     timing: bool = False                    # record per-item compute events
     end: bool = False                       # session end: followers return
     stop: bool = False                      # shut the follower down
+
+
+# ---------------------------------------------------------------------------
+# Binary wire format of the control plane (dist mode: rank 0 -> every rank)
+# ---------------------------------------------------------------------------
+# A plan travels as ONE fixed-size int32 record of PLAN_WORDS words (a gloo
+# message must be received into a buffer of the exact size):
+#   REPEAT  [magic, step]                         same groups as the previous
+#                                                 plan to this rank, step + 1
+#   STEADY  [magic, step, replica, flags, G,      decode-only groups (no
+#            (g, ret, n, b, ctxb) x G]            composition change, no chunk)
+#   PICKLE  [magic, nbytes]                       a pickled StepPlan follows as
+#                                                 a second message (joins,
+#                                                 leaves, prefill chunks, compat)
+# In steady-state decode every step is REPEAT or STEADY: no pickling, one
+# 512-byte message per follower.  The reference's control "plane" is a JSON
+# POST per token per shard (`/root/reference/server.py:172-181`).
+PLAN_WORDS = 128
+MAGIC_REPEAT, MAGIC_STEADY, MAGIC_PICKLE = 0x4C534452, 0x4C534453, 0x4C534450
+_MAX_STEADY_GROUPS = (PLAN_WORDS - 5) // 5
+_F_TIMING, _F_END, _F_STOP = 1, 2, 4
+
+
+def _steady_groups(plan: StepPlan):
+    """(g, ret, n, b, ctxb) per group when the plan is decode-only, else None."""
+    out = []
+    for gp in plan.groups:
+        if gp.rows is not None or gp.chunks or gp.kind != "step":
+            return None
+        out.append((gp.g, gp.ret, gp.n, gp.b, gp.ctxb))
+    return out if len(out) <= _MAX_STEADY_GROUPS else None
+
+
+class PlanEncoder:
+    """Per-destination encoder (remembers what it sent last for REPEAT)."""
+
+    def __init__(self):
+        self._prev = None  # (step, replica, flags, groups) of the last plan sent
+
+    def encode(self, plan: StepPlan):
+        """-> (int32 numpy record, pickle payload bytes or None)."""
+        import numpy as np
+
+        rec = np.zeros(PLAN_WORDS, dtype=np.int32)
+        flags = (_F_TIMING if plan.timing else 0) | (_F_END if plan.end else 0) | (_F_STOP if plan.stop else 0)
+        groups = _steady_groups(plan)
+        if groups is None:
+            import pickle
+
+            payload = pickle.dumps(plan, protocol=pickle.HIGHEST_PROTOCOL)
+            rec[0], rec[1] = MAGIC_PICKLE, len(payload)
+            self._prev = None
+            return rec, payload
+        prev = self._prev
+        if (prev is not None and plan.step == prev[0] + 1 and plan.replica == prev[1]
+                and flags == prev[2] and groups == prev[3] and groups):
+            rec[0], rec[1] = MAGIC_REPEAT, plan.step
+        else:
+            rec[0], rec[1], rec[2], rec[3], rec[4] = MAGIC_STEADY, plan.step, plan.replica, flags, len(groups)
+            if groups:
+                rec[5: 5 + 5 * len(groups)] = np.asarray(groups, dtype=np.int32).reshape(-1)
+        self._prev = (plan.step, plan.replica, flags, groups)
+        return rec, None
+
+
+class PlanDecoder:
+    """Per-source decoder (holds the previous plan's groups for REPEAT)."""
+
+    def __init__(self):
+        self._prev = None  # (replica, flags, groups)
+
+    def decode(self, rec, fetch_payload) -> StepPlan:
+        """rec: int32 sequence of PLAN_WORDS; fetch_payload(nbytes) -> bytes."""
+        magic = int(rec[0])
+        if magic == MAGIC_PICKLE:
+            import pickle
+
+            self._prev = None
+            # our own plan records, produced by this job's rank 0
+            return pickle.loads(fetch_payload(int(rec[1])))
+        if magic == MAGIC_REPEAT:
+            if self._prev is None:
+                raise ValueError("plan REPEAT record without a previous plan")
+            replica, flags, groups = self._prev
+            step = int(rec[1])
+        elif magic == MAGIC_STEADY:
+            step, replica, flags, G = (int(x) for x in rec[1:5])
+            vals = [int(x) for x in rec[5: 5 + 5 * G]]
+            groups = [tuple(vals[5 * i: 5 * i + 5]) for i in range(G)]
+            self._prev = (replica, flags, groups)
+        else:
+            raise ValueError(f"bad plan record magic {magic:#x}")
+        # fresh GroupPlan objects every step (workers key posted receives by id)
+        return StepPlan(step=step, replica=replica, timing=bool(flags & _F_TIMING),
+                        end=bool(flags & _F_END), stop=bool(flags & _F_STOP),
+                        groups=[GroupPlan(g, ret=r, n=n, b=b, ctxb=c) for g, r, n, b, c in groups])
