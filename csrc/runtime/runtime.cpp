@@ -18,12 +18,16 @@
 //                        admission into slots, per-step group plans (leaves,
 //                        joins, prefill chunks, decode rows / buckets), token
 //                        readout events and slot release.
+//   * ShmRing         -- one-node control plane (shm_ring.h): rank 0 writes a
+//                        step plan once into shared memory, every follower
+//                        rank of the pipeline replica reads it.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include "batch_queue.h"
 #include "sched_core.h"
+#include "shm_ring.h"
 
 #include <algorithm>
 #include <cmath>
@@ -123,4 +127,31 @@ PYBIND11_MODULE(_runtime, m) {
       .def_property_readonly("n_waiting", &SchedCore::n_waiting)
       .def_property_readonly("n_seqs", &SchedCore::n_seqs)
       .def_property_readonly("n_expect", &SchedCore::n_expect);
+  using lsd_rt::ShmRing;
+  py::class_<ShmRing>(m, "ShmRing")
+      .def_static("create", &ShmRing::create, py::arg("name"), py::arg("slots"), py::arg("slot_bytes"),
+                  py::arg("readers"), py::return_value_policy::take_ownership)
+      .def_static("attach", &ShmRing::attach, py::arg("name"), py::arg("index"),
+                  py::return_value_policy::take_ownership)
+      .def("publish", [](ShmRing& r, py::bytes b, double timeout_s) {
+             std::string s = b;
+             py::gil_scoped_release nogil;
+             return r.publish(s.data(), s.size(), timeout_s);
+           }, py::arg("data"), py::arg("timeout_s"))
+      .def("read", [](ShmRing& r, double timeout_s) -> py::object {
+             std::string out;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = r.read(&out, timeout_s);
+             }
+             if (!ok) return py::none();
+             return py::bytes(out);
+           }, py::arg("timeout_s"))
+      .def("unlink", &ShmRing::unlink)
+      .def("close", &ShmRing::close_ring)
+      .def_property_readonly("head", &ShmRing::head)
+      .def("cursor", &ShmRing::cursor)
+      .def_property_readonly("slots", &ShmRing::slots)
+      .def_property_readonly("slot_bytes", &ShmRing::slot_bytes);
 }

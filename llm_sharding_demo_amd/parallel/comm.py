@@ -459,6 +459,10 @@ class LocalPlanChannel:
     def send(self, dst: int, obj) -> None:
         self.q[dst].put(obj)
 
+    def send_many(self, dsts: List[int], obj) -> None:
+        for d in dsts:
+            self.q[d].put(obj)
+
     def recv(self, me: int, timeout: Optional[float] = None):
         return self.q[me].get(timeout=timeout)
 
@@ -515,6 +519,10 @@ class GlooPlanChannel:
         while self._works and all(x.is_completed() for x in self._works[0][0::2]):
             self._works.popleft()
 
+    def send_many(self, dsts: List[int], obj) -> None:
+        for d in dsts:
+            self.send(d, obj)
+
     def recv(self, src: int):
         if self.plans:
             from ..runtime.plan import PLAN_WORDS, PlanDecoder
@@ -541,6 +549,124 @@ class GlooPlanChannel:
             for x in w[0::2]:
                 x.wait()
         self._works.clear()
+
+
+class ShmPlanChannel:
+    """One-node control plane: each pipeline replica's step plans go through a
+    shared-memory broadcast ring (csrc/runtime/shm_ring.h) that rank 0 writes
+    ONCE per step and every follower rank of the replica reads -- instead of
+    one gloo message per follower per step (~20 us of rank 0's host time
+    each).  Records are runtime/plan.py's binary plans; a pickled plan rides
+    inline behind its record when it fits a slot, else over the gloo plan
+    group.  Every rank of an 8-GPU MI355X node shares the host, so this is
+    the default whenever torchrun reports one node (LOCAL_WORLD_SIZE ==
+    WORLD_SIZE); `GlooPlanChannel` otherwise."""
+
+    INLINE, VIA_GLOO = b"I", b"G"
+
+    def __init__(self, transport: "_DistTransport", timeout_s: float, slots: int = 64,
+                 slot_bytes: int = 4 << 20):
+        import secrets
+
+        from ..runtime import native
+
+        rt = native.load()
+        if rt is None or not hasattr(rt, "ShmRing"):
+            raise TransportError("native runtime with ShmRing not built")
+        self.P, self.R, self.grank = transport.P, transport.R, transport.grank
+        self.timeout_s = timeout_s
+        token = transport.broadcast_object(secrets.token_hex(6) if self.grank == 0 else None, src=0)
+        names = [f"/lsd-plan-{token}-r{rep}" for rep in range(self.R)]
+        self.readers = [[rep * self.P + s for s in range(self.P) if rep * self.P + s != 0]
+                        for rep in range(self.R)]
+        self.rings: Dict[int, object] = {}
+        self.ring = None
+        err = None
+        if self.grank == 0:
+            try:
+                for rep in range(self.R):
+                    if self.readers[rep]:
+                        self.rings[rep] = rt.ShmRing.create(names[rep], slots, slot_bytes,
+                                                            len(self.readers[rep]))
+            except Exception as e:  # noqa: BLE001 - every rank must learn the outcome
+                err = f"{type(e).__name__}: {e}"
+        err = transport.broadcast_object(err, src=0)
+        if err is None and self.grank != 0:
+            rep = self.grank // self.P
+            try:
+                self.ring = rt.ShmRing.attach(names[rep], self.readers[rep].index(self.grank))
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {self.grank}: {type(e).__name__}: {e}"
+        errs = transport.gather_object(err, dst=0)
+        errs = transport.broadcast_object([e for e in (errs or []) if e], src=0)
+        if self.grank == 0:
+            for r in self.rings.values():
+                r.unlink()  # every reader is attached: the mappings outlive the names
+        if err or errs:
+            raise TransportError(f"shared-memory plan ring unavailable: {err or errs}")
+        from ..runtime.plan import PlanDecoder, PlanEncoder
+
+        self._enc = {rep: PlanEncoder() for rep in self.rings}
+        self._dec = PlanDecoder()
+        self.fallback = GlooPlanChannel(transport.plan_pg, tag=1, plans=False)
+        self.bytes_sent = 0
+        self.msgs_sent = 0
+
+    def send_many(self, dsts: List[int], obj) -> None:
+        """Publish `obj` (a StepPlan) to the ring whose readers are `dsts`."""
+        if not dsts:
+            return
+        rep = dsts[0] // self.P
+        if sorted(dsts) != self.readers[rep]:
+            raise ValueError(f"plan destinations {dsts} are not replica {rep}'s followers")
+        rec, payload = self._enc[rep].encode(obj)
+        ring = self.rings[rep]
+        body = rec.tobytes()
+        if payload is None or len(payload) + len(body) + 1 <= ring.slot_bytes - 4:
+            data = self.INLINE + body + (payload or b"")
+            via = False
+        else:
+            data, via = self.VIA_GLOO + body, True
+        if not ring.publish(data, self.timeout_s):
+            raise TransportError(f"plan ring of replica {rep}: followers {self.timeout_s:.0f} s behind")
+        self.bytes_sent += len(data)
+        self.msgs_sent += 1
+        if via:
+            for d in dsts:
+                self.fallback.send(d, payload)
+
+    def send(self, dst: int, obj) -> None:
+        raise TypeError("ShmPlanChannel broadcasts per replica: use send_many")
+
+    def recv(self, src: int):
+        from ..runtime.plan import PLAN_WORDS
+
+        while True:  # an idle server waits here indefinitely
+            data = self.ring.read(1.0)
+            if data is not None:
+                break
+        import numpy as np
+
+        nrec = 4 * PLAN_WORDS
+        rec = np.frombuffer(data[1: 1 + nrec], dtype=np.int32)
+        if data[:1] == self.INLINE:
+            return self._dec.decode(rec, lambda n: data[1 + nrec: 1 + nrec + n])
+        return self._dec.decode(rec, lambda n: self.fallback.recv(0))
+
+    def flush(self) -> None:
+        self.fallback.flush()
+
+
+def make_plan_channel(transport: "_DistTransport", timeout_s: float):
+    """Shared-memory rings on one node, gloo records otherwise
+    (LSD_PLAN_WIRE = shm | binary | pickle)."""
+    import os
+
+    wire = os.environ.get("LSD_PLAN_WIRE", "shm")
+    one_node = os.environ.get("LOCAL_WORLD_SIZE", "") == os.environ.get("WORLD_SIZE", "-")
+    if wire == "shm" and one_node:
+        return ShmPlanChannel(transport, timeout_s)
+    return GlooPlanChannel(transport.plan_pg, tag=1, plans=wire != "pickle")
 
 
 # ---------------------------------------------------------------------------

@@ -40,7 +40,8 @@ from ..config import EngineConfig, SamplingParams
 from ..utils import racecheck
 from ..models.stage import StageModel
 from ..parallel.comm import (DeviceLoopFabric, GlooPlanChannel, LocalFabric, LocalPlanChannel,
-                             Transport, TransportError, init_distributed, make_dist_transport)
+                             Transport, TransportError, init_distributed, make_dist_transport,
+                             make_plan_channel)
 from ..parallel.partition import make_alt_unit_plans, make_unit_plan, union_plan, units_to_layers
 from ..parallel.pipeline import StageWorker
 from .kv_cache import KVCache, SlotAllocator, plan_slots
@@ -175,9 +176,9 @@ class Engine(racecheck.Shared):
             self.stages = [stage]
             self.workers = [self._worker(stage, self.transport, self.stage_idx)]
             self.fabric = None
-            # LSD_PLAN_WIRE=pickle: the pre-binary control plane (A/B only)
-            self.plan_ch = GlooPlanChannel(self.transport.plan_pg, tag=1,
-                                           plans=os.environ.get("LSD_PLAN_WIRE", "binary") != "pickle")
+            # step plans: shared-memory ring per replica on one node, binary
+            # gloo records otherwise (LSD_PLAN_WIRE=shm|binary|pickle)
+            self.plan_ch = make_plan_channel(self.transport, cfg.round_timeout_s)
             self.tok_ch = GlooPlanChannel(self.transport.tok_pg, tag=3, plans=False)
             self._tok_threads: List[threading.Thread] = []
             if self.rank == 0:
@@ -377,11 +378,9 @@ class Engine(racecheck.Shared):
         for rep in range(self.R):
             p = plans[rep] if plans is not None else StepPlan(step=-1, replica=rep, end=True,
                                                                timing=self.scheduler.timing)
-            for r in range(self.P):
-                g = rep * self.P + r
-                if g == 0:
-                    continue
-                self.plan_ch.send(g if self.mode == "dist" else r, p)
+            dsts = [rep * self.P + r if self.mode == "dist" else r for r in range(self.P)
+                    if rep * self.P + r != 0]
+            self.plan_ch.send_many(dsts, p)
 
     def _drive(self, until, timing: bool = False) -> None:
         """Run pipeline steps until `until()` (and no work is left in flight
@@ -652,12 +651,14 @@ class Engine(racecheck.Shared):
     def shutdown(self) -> None:
         self.stop_loop()
         if self.mode == "local":
-            for i in range(1, self.P):
-                self.plan_ch.send(i, StepPlan(step=-1, stop=True))
+            self.plan_ch.send_many(list(range(1, self.P)), StepPlan(step=-1, stop=True))
+            if self.watchdog is not None:
+                self.watchdog.close()
             return
         if self.rank == 0:
-            for r in range(1, self.P * self.R):
-                self.plan_ch.send(r, StepPlan(step=-1, stop=True))
+            for rep in range(self.R):
+                self.plan_ch.send_many([g for g in range(rep * self.P, (rep + 1) * self.P) if g],
+                                       StepPlan(step=-1, stop=True))
             self.plan_ch.flush()
             self._close_dist()
 
@@ -724,10 +725,8 @@ class Engine(racecheck.Shared):
             w0 = self.workers[0]
             gp = GroupPlan(0, kind="fwd_b", fwd_rows=T)
             plan = StepPlan(step=-2, groups=[gp])
-            for r in range(1, self.P):
-                self.plan_ch.send(r, plan)
-            for r in range(1, self.P):
-                self.plan_ch.send(r, StepPlan(step=-1, end=True))
+            self.plan_ch.send_many(list(range(1, self.P)), plan)
+            self.plan_ch.send_many(list(range(1, self.P)), StepPlan(step=-1, end=True))
             dev = self.devices[0]
             x = h.to(dev).contiguous()
             w0._send(x, 1, "fwd", 0).wait()  # in the wire dtype stage 1 expects

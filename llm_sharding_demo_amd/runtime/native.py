@@ -17,6 +17,7 @@ ROOT = os.path.dirname(PKG)
 SRC = os.path.join(ROOT, "csrc", "runtime", "runtime.cpp")
 HDR = os.path.join(ROOT, "csrc", "runtime", "batch_queue.h")
 CORE = os.path.join(ROOT, "csrc", "runtime", "sched_core.h")
+SHM = os.path.join(ROOT, "csrc", "runtime", "shm_ring.h")
 
 
 def build(force: bool = False) -> str:
@@ -28,14 +29,14 @@ def build(force: bool = False) -> str:
     flags = ["-O2", "-std=c++17", "-fPIC", "-shared", f"-I{pybind11.get_include()}",
              f"-I{sysconfig.get_paths()['include']}"]
     h = hashlib.sha1(" ".join(flags).encode())
-    for src in (SRC, HDR, CORE):
+    for src in (SRC, HDR, CORE, SHM):
         with open(src, "rb") as f:
             h.update(f.read())
     sig = h.hexdigest()
     if not force and os.path.exists(so) and os.path.exists(stamp) and open(stamp).read() == sig:
         return so
     tmp = so + ".tmp"
-    r = subprocess.run(["g++"] + flags + [SRC, "-o", tmp], capture_output=True, text=True)
+    r = subprocess.run(["g++"] + flags + [SRC, "-o", tmp, "-lrt"], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"runtime build failed:\n{r.stderr}")
     os.replace(tmp, so)

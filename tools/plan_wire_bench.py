@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch.distributed as dist  # noqa: E402
 
-from llm_sharding_demo_amd.parallel.comm import GlooPlanChannel  # noqa: E402
+from llm_sharding_demo_amd.parallel.comm import GlooPlanChannel, ShmPlanChannel  # noqa: E402
 from llm_sharding_demo_amd.runtime.plan import GroupPlan, StepPlan  # noqa: E402
 
 
@@ -25,8 +25,27 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     pg = dist.new_group(list(range(world)), backend="gloo")
-    for wire in ("pickle", "binary"):
-        ch = GlooPlanChannel(pg, tag=1, plans=True) if wire == "binary" else GlooPlanChannel(pg, tag=1, plans=False)
+    pg2 = dist.new_group(list(range(world)), backend="gloo")
+    class T:  # the transport surface ShmPlanChannel uses
+        P, R, grank, plan_pg = world, 1, rank, pg
+
+        @staticmethod
+        def broadcast_object(o, src=0):
+            lst = [o]
+            dist.broadcast_object_list(lst, src=src)
+            return lst[0]
+
+        @staticmethod
+        def gather_object(o, dst=0):
+            out = [None] * world if rank == dst else None
+            dist.gather_object(o, out, dst=dst)
+            return out
+
+    for wire in ("pickle", "binary", "shm"):
+        if wire == "shm":
+            ch = ShmPlanChannel(T, 60.0)
+        else:
+            ch = GlooPlanChannel(pg, tag=1, plans=wire == "binary")
         dist.barrier()
         if rank == 0:
             t_send, b0 = 0.0, ch.bytes_sent
@@ -35,26 +54,24 @@ def main():
                 plan = StepPlan(step=s, groups=[GroupPlan(g, ret=256, n=256, b=256, ctxb=256)
                                                 for g in range(G)])
                 t0 = time.perf_counter()
-                for r in range(1, world):
-                    ch.send(r, plan)
+                ch.send_many(list(range(1, world)), plan)
                 t_send += time.perf_counter() - t0
-                if s % 64 == 63:
-                    ch.flush()  # keep rank 0 at most 64 steps ahead (the engine's readout lag)
-            ch.send_stop = None
-            for r in range(1, world):
-                ch.send(r, StepPlan(step=-1, stop=True))
+                if s % 32 == 31:
+                    ch.flush()  # keep rank 0 at most 32 steps ahead (the engine's readout lag)
+                    dist.barrier(group=pg2)
+            ch.send_many(list(range(1, world)), StepPlan(step=-1, stop=True))
             ch.flush()
             print(f"{wire:6s} G={G} world={world}: send {t_send / steps * 1e6:7.1f} us/step "
                   f"({(ch.bytes_sent - b0) / (steps + 1):.0f} B/step to {world - 1} followers)", flush=True)
         else:
-            t_dec, n = 0.0, 0
+            n = 0
             while True:
-                t0 = time.perf_counter()
                 p = ch.recv(0)
-                t_dec += time.perf_counter() - t0
-                n += 1
                 if p.stop:
                     break
+                n += 1
+                if n % 32 == 0:
+                    dist.barrier(group=pg2)
         dist.barrier()
     dist.destroy_process_group()
 
