@@ -129,6 +129,21 @@ class _CaptureGate(racecheck.Shared):
 GPU_GATE = _CaptureGate()
 
 
+def wait_event(ev) -> None:
+    """Block until `ev` completed without holding GPU_GATE across the wait:
+    each query holds the gate (HIP refuses event queries during a sibling
+    thread's capture), the sleeps between them do not, so a sibling's
+    capture -- and, behind the writer-preferring gate, every other stage's
+    issue -- never waits for this thread's GPU wait."""
+    pause = 20e-6
+    while True:
+        with GPU_GATE.shared():
+            if ev.query():
+                return
+        time.sleep(pause)
+        pause = min(2 * pause, 200e-6)
+
+
 def prefill_chunks(lens: List[int], chunk: int) -> List[Tuple[List[int], List[int]]]:
     """(starts, qlens) per prefill chunk for prompts of `lens` tokens, aligned
     to the END of each prompt: the last chunk holds every sequence's final

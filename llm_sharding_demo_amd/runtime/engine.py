@@ -592,10 +592,9 @@ class Engine(racecheck.Shared):
                 return
             step, key, host, ev = item
             if ev is not None:
-                from ..parallel.pipeline import GPU_GATE
+                from ..parallel.pipeline import wait_event
 
-                with GPU_GATE.shared():  # not beside a stage thread's capture
-                    ev.synchronize()
+                wait_event(ev)  # queries gated against a stage thread's capture
             if delay:
                 time.sleep(delay)
             self.tok_ch.send(0, (step, key, host.tolist()))

@@ -575,7 +575,7 @@ class Scheduler(racecheck.Shared):
         key = (plan.replica, plan.step, gp.g)
         n = gp.ret
         if ret.is_cuda:
-            from ..parallel.pipeline import GPU_GATE
+            from ..parallel.pipeline import GPU_GATE, wait_event
 
             host = torch.empty(n, dtype=torch.int32, pin_memory=True)
             host.copy_(ret[:n], non_blocking=True)
@@ -591,8 +591,7 @@ class Scheduler(racecheck.Shared):
                     return ev.query()
 
             def sync(ev=ev):
-                with GPU_GATE.shared():
-                    ev.synchronize()
+                wait_event(ev)
             self.readouts.append((plan.step, ready, sync, host, key, None))
         else:
             host = ret[:n].clone()
@@ -603,15 +602,14 @@ class Scheduler(racecheck.Shared):
         previous token-return vector into `host` and its completion event
         `ev` are already enqueued (csrc/stage_exec.cpp); `release(ev)` hands
         the event back to the worker's pool once the readout is applied."""
-        from ..parallel.pipeline import GPU_GATE
+        from ..parallel.pipeline import GPU_GATE, wait_event
 
         def ready(ev=ev):
             with GPU_GATE.shared():
                 return ev.query()
 
         def sync(ev=ev):
-            with GPU_GATE.shared():
-                ev.synchronize()
+            wait_event(ev)
         self.readouts.append((plan.step, ready, sync, host, (plan.replica, plan.step, gp.g),
                               lambda ev=ev: release(ev)))
 
