@@ -576,7 +576,10 @@ class ShmPlanChannel:
         self.P, self.R, self.grank = transport.P, transport.R, transport.grank
         self.timeout_s = timeout_s
         token = transport.broadcast_object(secrets.token_hex(6) if self.grank == 0 else None, src=0)
-        names = [f"/lsd-plan-{token}-r{rep}" for rep in range(self.R)]
+        import os
+
+        prefix = os.environ.get("LSD_SHM_PREFIX", "/lsd-plan")
+        names = [f"{prefix}-{token}-r{rep}" for rep in range(self.R)]
         self.readers = [[rep * self.P + s for s in range(self.P) if rep * self.P + s != 0]
                         for rep in range(self.R)]
         self.rings: Dict[int, object] = {}
@@ -662,10 +665,18 @@ def make_plan_channel(transport: "_DistTransport", timeout_s: float):
     (LSD_PLAN_WIRE = shm | binary | pickle)."""
     import os
 
+    import logging
+
     wire = os.environ.get("LSD_PLAN_WIRE", "shm")
     one_node = os.environ.get("LOCAL_WORLD_SIZE", "") == os.environ.get("WORLD_SIZE", "-")
     if wire == "shm" and one_node:
-        return ShmPlanChannel(transport, timeout_s)
+        try:
+            return ShmPlanChannel(transport, timeout_s)
+        except TransportError as e:
+            # every rank saw the same error list (gathered + broadcast), so
+            # all of them fall back together
+            logging.getLogger("llm_sharding_demo_amd.comm").warning(
+                "shared-memory plan ring unavailable (%s): plans over gloo", e)
     return GlooPlanChannel(transport.plan_pg, tag=1, plans=wire != "pickle")
 
 

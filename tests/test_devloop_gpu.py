@@ -208,3 +208,15 @@ def test_devloop_stall_aborts_spinning_lanes():
     assert err == 1, err  # LOOP_ERR_ABORT: a device wait saw the abort word
     with pytest.raises(RuntimeError, match="unhealthy"):
         e.generate_ids([[1]], SamplingParams(greedy=True, max_new_tokens=1))
+    # advisor r3: nothing may launch on an aborted data plane -- a cached
+    # graph-I/O decode graph is refused, as are the eager ops
+    from llm_sharding_demo_amd.parallel.comm import TransportError
+
+    w = e.workers[1]
+    cached = [(gs, k) for gs in w.groups.values() for k in gs.graph_io if k in gs.graphs]
+    assert cached
+    gs, key = cached[0]
+    with pytest.raises(TransportError):
+        w._replay(gs, key, gs.graphs[key][0])
+    with pytest.raises(TransportError):
+        w.t.send(torch.zeros(4, device="cuda"), 0, "ret", 0)

@@ -181,3 +181,14 @@ def test_gloo_twin_stall_fails_within_deadline(tmp_path):
                         env_extra={"LSD_TEST_STALL_RANK": "1", "LSD_TEST_STALL_AFTER": "5"})
     assert res["err"] is not None and not res["healthy"], res
     assert res["elapsed"] < 4.0 + 30.0, res
+
+
+def test_gloo_twin_plan_ring_failure_falls_back(tmp_path):
+    """A node without usable shared memory (here: an invalid segment name)
+    falls back to the gloo plan records on every rank together."""
+    res, evid, r = _run(tmp_path, 2, "cpu", "gloo", greedy=False, timeout=300,
+                        env_extra={"LSD_SHM_PREFIX": "/no/such/dir"})
+    assert res["err"] is None, (res, r.stderr[-4000:])
+    assert "plans over gloo" in r.stderr
+    want = _one_stage("cpu", 1, greedy=False)
+    assert res["out"] == want
