@@ -57,8 +57,11 @@ __device__ __forceinline__ void set_err(LoopStatus* st, u32 code, u32 chan) {
 }
 
 // Ring placement: a message occupies [off, off + bytes) of the monotonic byte
-// stream and never straddles the ring's end (it skips to the next lap).
+// stream, starts 256-B aligned (16-B vector copies on both ends; the ring
+// itself is 256-B aligned) and never straddles the ring's end (it skips to
+// the next lap).  The host handshake mirrors this function exactly.
 __device__ __host__ __forceinline__ u64 place(u64 head, u64 bytes, u64 cap) {
+  head = (head + 255) & ~(u64)255;
   const u64 o = head % cap;
   return (o + bytes > cap) ? head + (cap - o) : head;
 }
