@@ -114,8 +114,8 @@ print(got, len(rc.reports()))
     assert out.strip() == "[3] 0"
 
 
-@pytest.mark.parametrize("P", [2, 3, 4])
-def test_multistage_engine_serving_is_race_free(P):
+@pytest.mark.parametrize("P,transport", [(2, "auto"), (3, "auto"), (4, "auto"), (3, "strict")])
+def test_multistage_engine_serving_is_race_free(P, transport):
     out = _run(f"""
 import threading
 from llm_sharding_demo_amd.utils import racecheck as rc
@@ -123,7 +123,8 @@ from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
 from llm_sharding_demo_amd.runtime.engine import Engine
 
 PROMPTS = [[5, 6, 7, 8], [11], [300, 2, 9], [1, 2], [40, 41, 42, 43, 44], [9, 9], [3], [77, 1]]
-eng = Engine(EngineConfig(model_id="gpt2-test", num_stages={P}, max_batch=8, device="cpu"))
+eng = Engine(EngineConfig(model_id="gpt2-test", num_stages={P}, max_batch=8, device="cpu",
+                          transport={transport!r}, num_microbatches=2))
 solo = eng.generate_ids(PROMPTS, SamplingParams(greedy=True, max_new_tokens=5))
 eng.start_loop()
 outs = [None] * len(PROMPTS)
@@ -160,8 +161,8 @@ print(e.round_started)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P", [2, 4])
-def test_loopback_gpu_engine_serving_is_race_free(P):
+@pytest.mark.parametrize("P,transport", [(2, "loopback"), (4, "loopback"), (3, "devloop")])
+def test_loopback_gpu_engine_serving_is_race_free(P, transport):
     """The same check on one MI355X: P stage threads with the device-async
     loopback transport, the capture gate shared by the stage threads, graph
     capture and replay, the serving loop and concurrent submitters."""
@@ -173,7 +174,7 @@ from llm_sharding_demo_amd.runtime.engine import Engine
 
 PROMPTS = [[i + 1, 2 * i + 3, 5] for i in range(12)]
 eng = Engine(EngineConfig(model_id="gpt2-test", num_stages={P}, max_batch=16, device="cuda",
-                          num_microbatches=2 * {P}, transport="loopback"))
+                          num_microbatches=2 * {P}, transport={transport!r}))
 eng.start_loop()
 outs = [None] * len(PROMPTS)
 def go(i):
