@@ -20,7 +20,7 @@ struct LoopChan {
   // constant after creation
   uint64_t cap;         // ring bytes
   uint64_t spin_limit;  // s_memrealtime ticks (100 MHz) a wait may last
-  uint8_t* ring;
+  uint8_t* ring;        // the owner's address (diagnostics only: kernels take theirs as an argument)
   uint32_t id, pad;
   // message headers: tag = seq + 1 once {size, off} and the payload are visible
   uint64_t h_tag[LOOP_HEADERS];

@@ -105,8 +105,10 @@ __device__ __forceinline__ void copy_part(uint8_t* dst, const uint8_t* src, u64 
   }
 }
 
-__global__ __launch_bounds__(THREADS) void loop_send_copy(LoopChan* ch, const uint8_t* src, u64 bytes,
-                                                          LoopStatus* st) {
+// `ring` is this process's address of the channel's ring (an IPC mapping when
+// the peer process owns it): pointers never travel through the shared state.
+__global__ __launch_bounds__(THREADS) void loop_send_copy(LoopChan* ch, uint8_t* ring, const uint8_t* src,
+                                                          u64 bytes, LoopStatus* st) {
   __shared__ u32 verdict;
   const u64 cap = ch->cap, nh = LOOP_HEADERS;
   const u64 seq = ch->s_seq, head = ch->s_off;  // sender-private: stream-ordered
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(THREADS) void loop_send_copy(LoopChan* ch, const ui
   }
   __syncthreads();
   if (verdict) return;
-  copy_part(ch->ring + off % cap, src, bytes);
+  copy_part(ring + off % cap, src, bytes);
 }
 
 __global__ void loop_send_publish(LoopChan* ch, u64 bytes) {
@@ -137,8 +139,8 @@ __global__ void loop_send_publish(LoopChan* ch, u64 bytes) {
   ch->s_off = off + bytes;
 }
 
-__global__ __launch_bounds__(THREADS) void loop_recv_copy(LoopChan* ch, uint8_t* dst, u64 bytes,
-                                                          LoopStatus* st) {
+__global__ __launch_bounds__(THREADS) void loop_recv_copy(LoopChan* ch, const uint8_t* ring, uint8_t* dst,
+                                                          u64 bytes, LoopStatus* st) {
   __shared__ u32 verdict;
   __shared__ u64 s_off;
   const u64 seq = ch->r_seq;  // receiver-private: stream-ordered
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(THREADS) void loop_recv_copy(LoopChan* ch, uint8_t*
   }
   __syncthreads();
   if (verdict) return;
-  copy_part(dst, ch->ring + s_off % ch->cap, bytes);
+  copy_part(dst, ring + s_off % ch->cap, bytes);
 }
 
 __global__ void loop_recv_release(LoopChan* ch) {
@@ -178,18 +180,18 @@ int copy_blocks(u64 bytes) {
 
 }  // namespace
 
-extern "C" hipError_t lsd_loop_send(LoopChan* ch, const void* src, uint64_t bytes, LoopStatus* st,
-                                    hipStream_t s) {
+extern "C" hipError_t lsd_loop_send(LoopChan* ch, void* ring, const void* src, uint64_t bytes,
+                                    LoopStatus* st, hipStream_t s) {
   hipLaunchKernelGGL(loop_send_copy, dim3(copy_blocks(bytes)), dim3(THREADS), 0, s, ch,
-                     static_cast<const uint8_t*>(src), bytes, st);
+                     static_cast<uint8_t*>(ring), static_cast<const uint8_t*>(src), bytes, st);
   hipLaunchKernelGGL(loop_send_publish, dim3(1), dim3(64), 0, s, ch, bytes);
   return hipGetLastError();
 }
 
-extern "C" hipError_t lsd_loop_recv(LoopChan* ch, void* dst, uint64_t bytes, LoopStatus* st,
-                                    hipStream_t s) {
+extern "C" hipError_t lsd_loop_recv(LoopChan* ch, const void* ring, void* dst, uint64_t bytes,
+                                    LoopStatus* st, hipStream_t s) {
   hipLaunchKernelGGL(loop_recv_copy, dim3(copy_blocks(bytes)), dim3(THREADS), 0, s, ch,
-                     static_cast<uint8_t*>(dst), bytes, st);
+                     static_cast<const uint8_t*>(ring), static_cast<uint8_t*>(dst), bytes, st);
   hipLaunchKernelGGL(loop_recv_release, dim3(1), dim3(64), 0, s, ch);
   return hipGetLastError();
 }

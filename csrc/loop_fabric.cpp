@@ -25,6 +25,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -40,26 +45,43 @@
 
 namespace py = pybind11;
 
-extern "C" hipError_t lsd_loop_send(LoopChan* ch, const void* src, uint64_t bytes, LoopStatus* st,
-                                    hipStream_t s);
-extern "C" hipError_t lsd_loop_recv(LoopChan* ch, void* dst, uint64_t bytes, LoopStatus* st,
-                                    hipStream_t s);
+extern "C" hipError_t lsd_loop_send(LoopChan* ch, void* ring, const void* src, uint64_t bytes,
+                                    LoopStatus* st, hipStream_t s);
+extern "C" hipError_t lsd_loop_recv(LoopChan* ch, const void* ring, void* dst, uint64_t bytes,
+                                    LoopStatus* st, hipStream_t s);
 extern "C" uint64_t lsd_loop_place(uint64_t head, uint64_t bytes, uint64_t cap);
 
 namespace {
 
 struct Fabric;
 
+// Enqueue mirrors of one channel (each side written by its one owning stage
+// thread / process): in process memory, or in a POSIX shared-memory block
+// when the two ends are different processes on one GPU (loop_chan_attach).
+struct alignas(64) Mirror {
+  std::atomic<uint64_t> send_n, send_end;
+  std::atomic<uint64_t> recv_n, recv_end;
+  // fault injection (tests): sends with index >= stall_from publish nothing
+  std::atomic<uint64_t> stall_from;
+};
+static_assert(sizeof(Mirror) == 64, "one cache line per channel mirror");
+
+void mirror_init(Mirror* m) {
+  m->send_n.store(0);
+  m->send_end.store(0);
+  m->recv_n.store(0);
+  m->recv_end.store(0);
+  m->stall_from.store(~0ull);
+}
+
 struct Chan {
   Fabric* fab = nullptr;
-  LoopChan* dev = nullptr;  // device state (torch-owned storage, kept alive by Python)
+  LoopChan* dev = nullptr;  // device state (torch-owned storage, or an IPC mapping)
+  uint8_t* ring = nullptr;  // this process's address of the ring
   uint64_t cap = 0;
   uint32_t id = 0;
-  // enqueue mirrors (each side written by its one owning stage thread)
-  std::atomic<uint64_t> send_n{0}, send_end{0};
-  std::atomic<uint64_t> recv_n{0}, recv_end{0};
-  // fault injection (tests): sends with index >= stall_from publish nothing
-  std::atomic<uint64_t> stall_from{~0ull};
+  Mirror* m = nullptr;      // own_m, or a slot of a shared-memory block
+  std::unique_ptr<Mirror> own_m;
 };
 
 struct Fabric {
@@ -110,8 +132,8 @@ void wait_ops(Fabric* f, const Ops& ops) {
                                " bytes exceeds the ring (" + std::to_string(c->cap) +
                                " bytes; raise LSD_LOOP_RING_MB)");
     // earlier ops of this list on the same channel and direction
-    uint64_t k = 0, head = op.dir ? c->recv_end.load(std::memory_order_relaxed)
-                                  : c->send_end.load(std::memory_order_relaxed);
+    uint64_t k = 0, head = op.dir ? c->m->recv_end.load(std::memory_order_relaxed)
+                                  : c->m->send_end.load(std::memory_order_relaxed);
     for (size_t j = 0; j < i; ++j)
       if (ops[j].ch == c && ops[j].dir == op.dir) {
         ++k;
@@ -120,11 +142,11 @@ void wait_ops(Fabric* f, const Ops& ops) {
     for (uint64_t spins = 0;; ++spins) {
       bool ok;
       if (op.dir) {  // receive #(recv_n + k) needs send #(recv_n + k) enqueued
-        ok = c->send_n.load(std::memory_order_acquire) > c->recv_n.load(std::memory_order_relaxed) + k;
+        ok = c->m->send_n.load(std::memory_order_acquire) > c->m->recv_n.load(std::memory_order_relaxed) + k;
       } else {  // send: header slot + ring bytes freed by already-enqueued receives
-        const uint64_t rn = c->recv_n.load(std::memory_order_acquire);
-        const uint64_t rend = c->recv_end.load(std::memory_order_acquire);
-        const uint64_t n = c->send_n.load(std::memory_order_relaxed) + k;
+        const uint64_t rn = c->m->recv_n.load(std::memory_order_acquire);
+        const uint64_t rend = c->m->recv_end.load(std::memory_order_acquire);
+        const uint64_t n = c->m->send_n.load(std::memory_order_relaxed) + k;
         const uint64_t off = lsd_loop_place(head, op.bytes, c->cap);
         ok = n - rn < LOOP_HEADERS && off + op.bytes - rend <= c->cap;
       }
@@ -148,24 +170,24 @@ void wait_ops(Fabric* f, const Ops& ops) {
 void launch_op(Fabric* f, const Op& op, void* ptr, hipStream_t st, bool mirror) {
   Chan* c = op.ch;
   if (op.dir == 0) {
-    const uint64_t n = c->send_n.load(std::memory_order_relaxed);
-    if (n >= c->stall_from.load(std::memory_order_relaxed)) {
+    const uint64_t n = c->m->send_n.load(std::memory_order_relaxed);
+    if (n >= c->m->stall_from.load(std::memory_order_relaxed)) {
       // fault injection: the message is never published; the peer's
       // receive kernel waits on device until the abort word or its deadline
     } else {
-      hip_check(lsd_loop_send(c->dev, ptr, op.bytes, f->dev, st), "loopback send");
+      hip_check(lsd_loop_send(c->dev, c->ring, ptr, op.bytes, f->dev, st), "loopback send");
     }
     if (mirror) {
-      const uint64_t end = lsd_loop_place(c->send_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
-      c->send_end.store(end, std::memory_order_relaxed);
-      c->send_n.store(n + 1, std::memory_order_release);
+      const uint64_t end = lsd_loop_place(c->m->send_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
+      c->m->send_end.store(end, std::memory_order_relaxed);
+      c->m->send_n.store(n + 1, std::memory_order_release);
     }
   } else {
-    hip_check(lsd_loop_recv(c->dev, ptr, op.bytes, f->dev, st), "loopback recv");
+    hip_check(lsd_loop_recv(c->dev, c->ring, ptr, op.bytes, f->dev, st), "loopback recv");
     if (mirror) {
-      const uint64_t end = lsd_loop_place(c->recv_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
-      c->recv_end.store(end, std::memory_order_release);
-      c->recv_n.store(c->recv_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
+      const uint64_t end = lsd_loop_place(c->m->recv_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
+      c->m->recv_end.store(end, std::memory_order_release);
+      c->m->recv_n.store(c->m->recv_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
     }
   }
 }
@@ -199,13 +221,13 @@ void lsd_loop_io_done(int64_t io) {
   for (const Op& op : l->ops) {
     Chan* c = op.ch;
     if (op.dir == 0) {
-      const uint64_t end = lsd_loop_place(c->send_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
-      c->send_end.store(end, std::memory_order_relaxed);
-      c->send_n.store(c->send_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
+      const uint64_t end = lsd_loop_place(c->m->send_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
+      c->m->send_end.store(end, std::memory_order_relaxed);
+      c->m->send_n.store(c->m->send_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
     } else {
-      const uint64_t end = lsd_loop_place(c->recv_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
-      c->recv_end.store(end, std::memory_order_release);
-      c->recv_n.store(c->recv_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
+      const uint64_t end = lsd_loop_place(c->m->recv_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
+      c->m->recv_end.store(end, std::memory_order_release);
+      c->m->recv_n.store(c->m->recv_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
     }
   }
 }
@@ -237,7 +259,11 @@ void lsd_register_loopback(py::module& m) {
     std::lock_guard<std::mutex> g(f->mu);
     auto c = std::make_unique<Chan>();
     c->fab = f;
+    c->own_m = std::make_unique<Mirror>();
+    c->m = c->own_m.get();
+    mirror_init(c->m);
     c->dev = reinterpret_cast<LoopChan*>(state.data_ptr());
+    c->ring = static_cast<uint8_t*>(ring.data_ptr());
     c->cap = (uint64_t)ring.numel();
     c->id = (uint32_t)f->chans.size();
     LoopChan init;
@@ -320,8 +346,79 @@ void lsd_register_loopback(py::module& m) {
   });
   m.def("loop_counts", [](int64_t chan) {
     Chan* c = as_chan(chan);
-    return std::make_tuple((int64_t)c->send_n.load(), (int64_t)c->recv_n.load(),
-                           (int64_t)c->send_end.load(), (int64_t)c->recv_end.load());
+    return std::make_tuple((int64_t)c->m->send_n.load(), (int64_t)c->m->recv_n.load(),
+                           (int64_t)c->m->send_end.load(), (int64_t)c->m->recv_end.load());
   });
-  m.def("loop_stall", [](int64_t chan, int64_t from) { as_chan(chan)->stall_from.store((uint64_t)from); });
+  m.def("loop_stall", [](int64_t chan, int64_t from) { as_chan(chan)->m->stall_from.store((uint64_t)from); });
+
+  // --- one GPU, several processes (dist-mode rehearsal, parallel/comm.py
+  // IpcLoopTransport): the receiving rank allocates its channels' state and
+  // ring with hipMalloc and exports them (hipIpcGetMemHandle, dmabuf); the
+  // sending rank maps them (hipIpcOpenMemHandle); both ends' enqueue mirrors
+  // live in one POSIX shared-memory block of 64-B slots.
+  m.def("loop_dev_alloc", [](int64_t bytes) {
+    void* p = nullptr;
+    hip_check(hipMalloc(&p, (size_t)bytes), "hipMalloc(loop)");
+    hip_check(hipMemset(p, 0, (size_t)bytes), "hipMemset(loop)");
+    return reinterpret_cast<int64_t>(p);
+  });
+  m.def("loop_dev_free", [](int64_t p) { hipFree(reinterpret_cast<void*>(p)); });
+  m.def("loop_ipc_handle", [](int64_t p) {
+    hipIpcMemHandle_t h;
+    hip_check(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(p)), "hipIpcGetMemHandle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  });
+  m.def("loop_ipc_open", [](py::bytes hb) {
+    const std::string s = hb;
+    if (s.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("bad IPC handle");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, s.data(), sizeof(h));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    return reinterpret_cast<int64_t>(p);
+  });
+  m.def("loop_shm_map", [](const std::string& name, int64_t bytes, bool create) {
+    int fd = shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+    if (fd < 0) throw std::runtime_error("shm_open(" + name + "): " + std::strerror(errno));
+    if (create && ftruncate(fd, (off_t)bytes) != 0) {
+      close(fd);
+      shm_unlink(name.c_str());
+      throw std::runtime_error("ftruncate(" + name + "): " + std::strerror(errno));
+    }
+    void* p = mmap(nullptr, (size_t)bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) throw std::runtime_error("mmap(" + name + "): " + std::strerror(errno));
+    return reinterpret_cast<int64_t>(p);  // mapped for the life of the process
+  });
+  m.def("loop_shm_unlink", [](const std::string& name) { shm_unlink(name.c_str()); });
+  // A channel over given device pointers and a shared mirror slot; the
+  // receiving end initialises the device state and the mirror (before any
+  // sender attaches).
+  m.def("loop_chan_attach", [](int64_t fab, int64_t state, int64_t ring, int64_t cap, int64_t id,
+                               int64_t mirror, bool init, double spin_limit_s) {
+    Fabric* f = as_fab(fab);
+    if (!state || !ring || !mirror || cap <= 0 || (ring & 255))
+      throw std::invalid_argument("loop_chan_attach: bad pointers");
+    std::lock_guard<std::mutex> g(f->mu);
+    auto c = std::make_unique<Chan>();
+    c->fab = f;
+    c->m = reinterpret_cast<Mirror*>(mirror);
+    c->dev = reinterpret_cast<LoopChan*>(state);
+    c->ring = reinterpret_cast<uint8_t*>(ring);
+    c->cap = (uint64_t)cap;
+    c->id = (uint32_t)id;
+    if (init) {
+      LoopChan st;
+      std::memset(&st, 0, sizeof(st));
+      st.cap = c->cap;
+      st.spin_limit = (uint64_t)(spin_limit_s * 1e8);
+      st.ring = reinterpret_cast<uint8_t*>(ring);
+      st.id = c->id;
+      hip_check(hipMemcpy(c->dev, &st, sizeof(st), hipMemcpyHostToDevice), "hipMemcpy(chan init)");
+      mirror_init(c->m);
+    }
+    Chan* raw = c.get();
+    f->chans.push_back(std::move(c));
+    return reinterpret_cast<int64_t>(raw);
+  });
 }

@@ -861,27 +861,19 @@ class DeviceLoopFabric(LocalFabric):
         return tuple(self.C.loop_counts(self.chan(edge, src, dst, lane)))
 
 
-class DeviceLoopTransport(Transport):
-    """One stage's view of a `DeviceLoopFabric`: the API of `RcclTransport`
-    (ops enqueued on the current stream, eagerly or inside a hipGraph
-    capture; handles already complete in stream order), so the pipeline
-    takes its graph-I/O path and the native executor exactly as over RCCL."""
+class _LoopOps:
+    """Data-plane ops over device loopback channels (csrc/loop_fabric.cpp),
+    with `RcclTransport`'s API: ops enqueued on the current stream, eagerly
+    or inside a hipGraph capture; handles already complete in stream order.
+    The subclass provides `C`, `_loop_aborted()` and `_chan(edge, src, dst,
+    lane)`."""
 
     GRAPH_IO = True
-
-    def __init__(self, fabric: DeviceLoopFabric, rank: int):
-        self.fabric, self.rank, self.world = fabric, rank, fabric.P
-        self.C = fabric.C
-        self._tls = threading.local()
-
-    @property
-    def aborted(self) -> bool:
-        return self.fabric.aborted
 
     def _op(self, ch: int, d: int, t: torch.Tensor) -> None:
         from .pipeline import GPU_GATE
 
-        if self.fabric.aborted:
+        if self._loop_aborted():
             raise TransportError("loopback data plane aborted")
         nbytes = t.numel() * t.element_size()
         ops = getattr(self._tls, "ops", None)
@@ -900,11 +892,11 @@ class DeviceLoopTransport(Transport):
     def send(self, t, dst, edge, lane=0):
         if not t.is_contiguous():
             t = t.contiguous()
-        self._op(self.fabric.chan(edge, self.rank, dst, lane), 0, t)
+        self._op(self._chan(edge, self.rank, dst, lane), 0, t)
         return SendHandle()
 
     def irecv(self, out, src, edge, lane=0):
-        ch = self.fabric.chan(edge, src, self.rank, lane)
+        ch = self._chan(edge, src, self.rank, lane)
         if out.is_contiguous():
             self._op(ch, 1, out)
             return Handle(out)
@@ -930,7 +922,7 @@ class DeviceLoopTransport(Transport):
         outside the capture gate (the step's ops in the native executor)."""
         from .pipeline import GPU_GATE
 
-        if self.fabric.aborted:
+        if self._loop_aborted():
             raise TransportError("loopback data plane aborted")
         if not ops:
             return
@@ -951,7 +943,28 @@ class DeviceLoopTransport(Transport):
 
     def native_recv(self, edge: str, src: int, lane: int) -> tuple:
         """("loop", channel) of a receive the native executor enqueues."""
-        return ("loop", self.fabric.chan(edge, src, self.rank, lane))
+        return ("loop", self._chan(edge, src, self.rank, lane))
+
+
+class DeviceLoopTransport(_LoopOps, Transport):
+    """One stage thread's view of a `DeviceLoopFabric` (P stage threads in
+    one process), so the pipeline takes its graph-I/O path and the native
+    executor exactly as over RCCL."""
+
+    def __init__(self, fabric: DeviceLoopFabric, rank: int):
+        self.fabric, self.rank, self.world = fabric, rank, fabric.P
+        self.C = fabric.C
+        self._tls = threading.local()
+
+    @property
+    def aborted(self) -> bool:
+        return self.fabric.aborted
+
+    def _loop_aborted(self) -> bool:
+        return self.fabric.aborted
+
+    def _chan(self, edge, src, dst, lane):
+        return self.fabric.chan(edge, src, dst, lane)
 
     def check_async(self) -> Optional[str]:
         return self.fabric.check_async()
@@ -964,6 +977,129 @@ class DeviceLoopTransport(Transport):
 
     def barrier(self) -> None:
         self.fabric._barrier.wait(timeout=self.fabric.timeout)
+
+
+class IpcLoopTransport(_LoopOps, _DistTransport):
+    """Dist mode (one process per stage, torch.distributed control plane) with
+    every rank on the SAME GPU and the pipeline edges on device loopback
+    channels shared between the processes: the single-GPU rehearsal of the
+    8-GPU `--transport rccl` run -- separate processes (no shared GIL, the
+    gloo / shared-memory control plane, worker_loop followers), decode graphs
+    with their own edge transfers, the native executor at P > 1.  Only the
+    RCCL byte mover itself is replaced (RCCL refuses two ranks on one GPU).
+
+    Channels: one per (replica, edge, lane), as `RcclTransport`'s
+    communicators.  The receiving rank allocates a channel's device state and
+    ring (hipMalloc) and exports them (hipIpcGetMemHandle); the sending rank
+    maps them.  Both ends' enqueue mirrors live in one POSIX shared-memory
+    block created by rank 0.  Each process keeps its own pinned abort / error
+    word (its watchdog aborts its own waits)."""
+
+    EDGE_GROUPS = False
+
+    def _backend(self) -> str:
+        return "gloo"
+
+    def __init__(self, num_stages: int, replicas: int = 1, lanes: int = 2,
+                 timeout_s: Optional[float] = None, ring_bytes: int = 64 << 20,
+                 ret_bytes: int = 16 << 20, spin_limit_s: float = 30.0):
+        import secrets
+
+        super().__init__(num_stages, replicas, timeout_s)
+        from ..ops.hip import _load
+
+        self.C = _load()
+        self.L = max(1, lanes)
+        self._tls = threading.local()
+        self.aborted = False
+        self.handle = self.C.loop_fabric_create(float(timeout_s or 600.0))
+        P, R = self.P, self.R
+        table = []  # (replica, edge, src stage, dst stage, lane): channel id = index
+        for rep in range(R):
+            for i in range(P - 1):
+                table += [(rep, "fwd", i, i + 1, l) for l in range(self.L)]
+            if P > 1:
+                table += [(rep, "ret", P - 1, 0, l) for l in range(self.L)]
+        token = self.broadcast_object(secrets.token_hex(6) if self.grank == 0 else None, src=0)
+        name = f"/lsd-loop-{token}"
+        nmir = max(1, len(table)) * 64
+        if self.grank == 0:
+            base = self.C.loop_shm_map(name, nmir, True)
+        self.barrier()
+        if self.grank != 0:
+            base = self.C.loop_shm_map(name, nmir, False)
+        self.barrier()
+        if self.grank == 0:
+            self.C.loop_shm_unlink(name)
+        nstate = self.C.loop_state_bytes()
+        self._own: List[int] = []
+        self.chans: Dict[tuple, int] = {}
+        exports = {}
+        for cid, (rep, edge, src, dst, lane) in enumerate(table):
+            if rep * P + dst != self.grank:
+                continue
+            cap = -(-(ring_bytes if edge == "fwd" else ret_bytes) // 256) * 256
+            st, ring = self.C.loop_dev_alloc(nstate), self.C.loop_dev_alloc(cap)
+            self._own += [st, ring]
+            self.chans[(edge, src, dst, lane)] = self.C.loop_chan_attach(
+                self.handle, st, ring, cap, cid, base + 64 * cid, True, float(spin_limit_s))
+            exports[cid] = (self.C.loop_ipc_handle(st), self.C.loop_ipc_handle(ring), cap)
+        torch.cuda.synchronize()
+        allx = self.gather_object(exports, dst=0)
+        merged = {}
+        for d in (allx or []):
+            merged.update(d or {})
+        merged = self.broadcast_object(merged, src=0)  # receivers initialised before senders attach
+        for cid, (rep, edge, src, dst, lane) in enumerate(table):
+            if rep * P + src != self.grank:
+                continue
+            hs, hr, cap = merged[cid]
+            st, ring = self.C.loop_ipc_open(hs), self.C.loop_ipc_open(hr)
+            self.chans[(edge, src, dst, lane)] = self.C.loop_chan_attach(
+                self.handle, st, ring, cap, cid, base + 64 * cid, False, float(spin_limit_s))
+        self.barrier()
+
+    @property
+    def num_comms(self) -> int:
+        return len(self.chans)
+
+    def _loop_aborted(self) -> bool:
+        return self.aborted
+
+    def _chan(self, edge, src, dst, lane):
+        return self.chans[(edge, src, dst, lane % self.L)]
+
+    def warmup(self, device) -> None:
+        """One exchange per channel in the global order, checking the data."""
+        for (edge, src, dst, lane) in sorted(self.chans, key=lambda k: (k[0] != "fwd", k[1], k[3])):
+            tag = float(src * self.L + lane + 1)
+            if src == self.rank:
+                self.send(torch.full((4,), tag, device=device), dst, edge, lane)
+            else:
+                got = torch.zeros(4, device=device)
+                self.irecv(got, src, edge, lane)
+                torch.cuda.synchronize(device)
+                if float(got[0].item()) != tag:
+                    raise TransportError(f"warmup on {edge} {src}->{dst} lane {lane}: got {got[0].item()}")
+        torch.cuda.synchronize(device)
+        self.barrier()
+
+    def check_async(self) -> Optional[str]:
+        if self.aborted:
+            return None
+        err, ch = self.C.loop_status(self.handle)
+        if err == 0:
+            return None
+        what = {1: "aborted", 2: "device wait timed out",
+                3: "receive size != message size (op order mismatch)"}
+        return f"loopback channel {ch}: {what.get(err, f'error {err}')}"
+
+    def abort(self) -> None:
+        self.aborted = True
+        self.C.loop_abort(self.handle)
+
+    def stall(self, edge: str, src: int, dst: int, lane: int, from_msg: int) -> None:
+        self.C.loop_stall(self._chan(edge, src, dst, lane), from_msg)
 
 
 class LocalTransport(Transport):
@@ -1096,6 +1232,15 @@ def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1,
         return t
     if kind == "nccl":
         t = NcclTransport(num_stages, replicas, timeout_s)
+        t.warmup(device)
+        return t
+    if kind == "devloop":  # every rank on one GPU: the 1-GPU rehearsal of "rccl"
+        import os
+
+        t = IpcLoopTransport(num_stages, replicas, lanes=int(os.environ.get("LSD_LANES", "2")),
+                             timeout_s=timeout_s,
+                             ring_bytes=int(os.environ.get("LSD_LOOP_RING_MB", "256")) << 20,
+                             spin_limit_s=float(os.environ.get("LSD_LOOP_SPIN_S", "30")))
         t.warmup(device)
         return t
     if kind == "gloo":

@@ -243,10 +243,22 @@ class Engine(racecheck.Shared):
             acc = per_dev.setdefault(str(dev), [dev, 0, 0])
             acc[1] += sum(1 for u in range(a, b) if u % 2 == 0)
             acc[2] += self._weight_bytes(si)
+        # dist ranks sharing one GPU (the single-GPU rehearsal of a multi-GPU
+        # run): each takes an equal share of the device's memory instead of a
+        # fraction of whatever the ranks initialised before it left free
+        share = None
+        if collective and torch.cuda.is_available():
+            import torch.distributed as dist
+
+            per_gpu = -(-dist.get_world_size() // max(1, torch.cuda.device_count()))
+            if per_gpu > 1:
+                def share(d, n=per_gpu):
+                    free, total = torch.cuda.mem_get_info(d)
+                    return min(free, int(total * 0.9) // n), total
         for dev, n_kv_layers, w_bytes in per_dev.values():
             fits = min(fits, plan_slots(want + 2, n_kv_layers, self.mcfg.n_kv_heads, self.max_seq,
                                         self.mcfg.head_dim, dev, reserve=w_bytes,
-                                        fraction=self.cfg.kv_fraction) - 2)
+                                        fraction=self.cfg.kv_fraction, mem_get_info=share) - 2)
         if collective:
             import torch.distributed as dist
 

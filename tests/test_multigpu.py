@@ -192,3 +192,31 @@ def test_gloo_twin_plan_ring_failure_falls_back(tmp_path):
     assert "plans over gloo" in r.stderr
     want = _one_stage("cpu", 1, greedy=False)
     assert res["out"] == want
+
+
+# ---------------------------------------------------------------------------
+# One GPU, several processes: the dist-mode rehearsal of the rccl data plane
+# (parallel/comm.py IpcLoopTransport: device loopback channels shared between
+# the rank processes, graph-captured transfers, native executor at P > 1)
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,dp", [(2, 1), (3, 1), (4, 2)])
+def test_devloop_processes_on_one_gpu_match_one_gpu(tmp_path, world, dp):
+    res, evid, r = _run(tmp_path, world, "cuda", "devloop", dp=dp, greedy=False, timeout=400,
+                        env_extra={"LSD_LOOP_RING_MB": "16"})
+    assert res["err"] is None, (res, r.stderr[-4000:])
+    assert res["world"] == world and res["healthy"]
+    assert res["out"] == _one_stage("cuda", 2 * world // dp, greedy=False) == res["out2"]
+    # every rank ran captured edge transfers and native steps
+    assert res["graph_io"] and res["native"] > 0, res
+    assert all(e["graph_io"] and e["native"] > 0 for e in evid), evid
+    assert all(e["io"] > 0 for e in evid if e["rank"] % (world // dp) != 0), evid
+
+
+@pytest.mark.gpu
+def test_devloop_processes_stall_fails_within_deadline(tmp_path):
+    res, evid, r = _run(tmp_path, 2, "cuda", "devloop", round_timeout=6.0, timeout=300,
+                        env_extra={"LSD_LOOP_RING_MB": "16", "LSD_TEST_STALL_RANK": "1",
+                                   "LSD_TEST_STALL_AFTER": "25"})
+    assert res["err"] is not None and not res["healthy"], res
+    assert res["elapsed"] < 6.0 + 30.0, res
