@@ -49,7 +49,9 @@ def parse():
     p.add_argument("--dp", type=int, default=int(os.environ.get("BENCH_DP", "1")),
                    help="pipeline replicas: N GPUs = (N/dp)-stage pipeline x dp (default 1: ppN)")
     p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),
-                   help="nccl (RCCL via torch.distributed) | rccl (native RCCL communicator, csrc/comm.cpp) | gloo (host-staged, for rehearsals)")
+                   help="nccl (RCCL via torch.distributed) | rccl (native RCCL communicator, csrc/comm.cpp) | "
+                        "gloo (host-staged, for rehearsals) | devloop (every rank on ONE GPU: device loopback "
+                        "channels between the rank processes, the rccl code path's rehearsal)")
     p.add_argument("--loopback-stages", type=int, default=0,
                    help="rehearsal: run this many pipeline stages as threads on ONE GPU; "
                         "--batch is then the total batch")
@@ -208,7 +210,8 @@ def main() -> int:
                        "prompt_len": args.prompt, "gen_tokens": args.gen, "microbatches": M,
                        "prefill_chunk": chunk,
                        "parallelism": f"pp{P}" + (f"xdp{R}" if R > 1 else "")
-                       + ("-loopback-1gpu" if args.loopback_stages else ""),
+                       + ("-loopback-1gpu" if args.loopback_stages else "")
+                       + ("-ranks-on-1gpu" if transport == "devloop" and N > 1 else ""),
                        "sampler": "greedy" if args.greedy else "T0.6/top-k40",
                        "hipgraphs": not args.no_graphs},
         }
