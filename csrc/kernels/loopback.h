@@ -22,6 +22,7 @@ struct LoopChan {
   uint64_t spin_limit;  // s_memrealtime ticks (100 MHz) a wait may last
   uint8_t* ring;        // the owner's address (diagnostics only: kernels take theirs as an argument)
   uint32_t id, pad;
+  uint64_t stall_from;  // fault injection (tests): messages >= this are never published
   // message headers: tag = seq + 1 once {size, off} and the payload are visible
   uint64_t h_tag[LOOP_HEADERS];
   uint64_t h_size[LOOP_HEADERS];

@@ -131,6 +131,7 @@ __global__ void loop_send_publish(LoopChan* ch, u64 bytes) {
   if (threadIdx.x != 0) return;
   const u64 cap = ch->cap;
   const u64 seq = ch->s_seq, off = place(ch->s_off, bytes, cap);
+  if (seq >= ch->stall_from) return;  // fault injection: the peer waits on the device
   const u32 k = (u32)(seq % LOOP_HEADERS);
   __hip_atomic_store(&ch->h_size[k], bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&ch->h_off[k], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

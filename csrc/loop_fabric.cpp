@@ -31,6 +31,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstddef>
 #include <chrono>
 #include <cstring>
 #include <memory>
@@ -171,12 +172,7 @@ void launch_op(Fabric* f, const Op& op, void* ptr, hipStream_t st, bool mirror) 
   Chan* c = op.ch;
   if (op.dir == 0) {
     const uint64_t n = c->m->send_n.load(std::memory_order_relaxed);
-    if (n >= c->m->stall_from.load(std::memory_order_relaxed)) {
-      // fault injection: the message is never published; the peer's
-      // receive kernel waits on device until the abort word or its deadline
-    } else {
-      hip_check(lsd_loop_send(c->dev, c->ring, ptr, op.bytes, f->dev, st), "loopback send");
-    }
+    hip_check(lsd_loop_send(c->dev, c->ring, ptr, op.bytes, f->dev, st), "loopback send");
     if (mirror) {
       const uint64_t end = lsd_loop_place(c->m->send_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
       c->m->send_end.store(end, std::memory_order_relaxed);
@@ -272,6 +268,7 @@ void lsd_register_loopback(py::module& m) {
     init.spin_limit = (uint64_t)(spin_limit_s * 1e8);  // s_memrealtime runs at 100 MHz
     init.ring = static_cast<uint8_t*>(ring.data_ptr());
     init.id = c->id;
+    init.stall_from = ~0ull;
     hip_check(hipMemcpy(c->dev, &init, sizeof(init), hipMemcpyHostToDevice), "hipMemcpy(chan init)");
     Chan* raw = c.get();
     f->chans.push_back(std::move(c));
@@ -349,7 +346,14 @@ void lsd_register_loopback(py::module& m) {
     return std::make_tuple((int64_t)c->m->send_n.load(), (int64_t)c->m->recv_n.load(),
                            (int64_t)c->m->send_end.load(), (int64_t)c->m->recv_end.load());
   });
-  m.def("loop_stall", [](int64_t chan, int64_t from) { as_chan(chan)->m->stall_from.store((uint64_t)from); });
+  // fault injection (tests, device idle): the send kernels stop publishing at
+  // message `from` of this channel -- eager or graph-replayed alike
+  m.def("loop_stall", [](int64_t chan, int64_t from) {
+    Chan* c = as_chan(chan);
+    const uint64_t v = (uint64_t)from;
+    hip_check(hipMemcpy(reinterpret_cast<char*>(c->dev) + offsetof(LoopChan, stall_from), &v, sizeof(v),
+                        hipMemcpyHostToDevice), "hipMemcpy(stall)");
+  });
 
   // --- one GPU, several processes (dist-mode rehearsal, parallel/comm.py
   // IpcLoopTransport): the receiving rank allocates its channels' state and
@@ -414,6 +418,7 @@ void lsd_register_loopback(py::module& m) {
       st.spin_limit = (uint64_t)(spin_limit_s * 1e8);
       st.ring = reinterpret_cast<uint8_t*>(ring);
       st.id = c->id;
+      st.stall_from = ~0ull;
       hip_check(hipMemcpy(c->dev, &st, sizeof(st), hipMemcpyHostToDevice), "hipMemcpy(chan init)");
       mirror_init(c->m);
     }
