@@ -207,10 +207,12 @@ def test_devloop_processes_on_one_gpu_match_one_gpu(tmp_path, world, dp):
     assert res["err"] is None, (res, r.stderr[-4000:])
     assert res["world"] == world and res["healthy"]
     assert res["out"] == _one_stage("cuda", 2 * world // dp, greedy=False) == res["out2"]
-    # every rank ran captured edge transfers and native steps
+    # every rank of replica 0 ran captured edge transfers and native steps (the
+    # scheduler may place all six requests on replica 0)
+    P = world // dp
     assert res["graph_io"] and res["native"] > 0, res
-    assert all(e["graph_io"] and e["native"] > 0 for e in evid), evid
-    assert all(e["io"] > 0 for e in evid if e["rank"] % (world // dp) != 0), evid
+    assert all(e["graph_io"] for e in evid), evid
+    assert all(e["native"] > 0 and e["io"] > 0 for e in evid if e["rank"] < P), evid
 
 
 @pytest.mark.gpu
