@@ -240,4 +240,16 @@ def main() -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    try:
+        rc = main()
+    except BaseException:  # noqa: BLE001
+        # a failed run may leave stage threads parked in native code (a
+        # data-plane wait, a stream synchronize); interpreter finalization
+        # would then abort the process -- report and leave without it
+        import traceback
+
+        traceback.print_exc()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(1)
+    sys.exit(rc)

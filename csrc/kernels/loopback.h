@@ -13,9 +13,11 @@ enum : uint32_t {
 };
 
 struct LoopChan {
-  // written by the sender's publish kernel only (stream-ordered)
+  // written by the sender's kernels only (stream-ordered)
   uint64_t s_seq, s_off;
-  // written by the receiver's release kernel only; polled by the sender
+  uint32_t s_verdict, r_verdict;  // a wait kernel's outcome for the copy / finish kernels behind it
+  uint64_t r_cur;                 // receiver: ring offset of the message being received
+  // written by the receiver's release only; polled by the sender
   uint64_t r_seq, r_off;
   // constant after creation
   uint64_t cap;         // ring bytes
