@@ -7,14 +7,14 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 step() { echo "== $(date +%T) $*"; }
 PHASE=${1:-tests}
-if [ "$PHASE" = tests ]; then
+if [ "$PHASE" = tests ] || [ "$PHASE" = both ]; then
 step tests
 timeout -k 10 700 python -u -m pytest tests/test_devloop_gpu.py tests/test_racecheck.py tests/test_multigpu.py -m gpu -v -x --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/r4_devloop_tests.log 2>&1
 rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/r4_devloop_tests.log | tail -40; [ $rc -eq 0 ] || exit $rc
 step bench
 timeout -k 10 400 python bench.py --steps 5 --warmup 2 > gpurun_out/r4_bench1.log 2>&1 || exit $?
 grep "^{" gpurun_out/r4_bench1.log
-exit 0
+[ "$PHASE" = both ] || exit 0
 fi
 export LSD_HOST_PROFILE=1
 L=gpurun_out/r4_rehearsal.log; : > $L
