@@ -158,7 +158,7 @@ def test_rccl_stall_abort_unblocks_recv(tmp_path):
     ncclCommAbort must return the receive, and the request must fail within
     the deadline."""
     res, evid, r = _run(tmp_path, 2, "cuda", "rccl", round_timeout=8.0, timeout=300,
-                        env_extra={"LSD_TEST_STALL_RANK": "1", "LSD_TEST_STALL_AFTER": "25"})
+                        env_extra={"LSD_TEST_STALL_RANK": "1", "LSD_TEST_STALL_AFTER": "8"})
     assert res["err"] is not None and not res["healthy"], res
     assert "WatchdogTimeout" in res["err"] or "abort" in res["err"], res["err"]
     assert res["elapsed"] < 8.0 + 30.0, res
@@ -219,6 +219,6 @@ def test_devloop_processes_on_one_gpu_match_one_gpu(tmp_path, world, dp):
 def test_devloop_processes_stall_fails_within_deadline(tmp_path):
     res, evid, r = _run(tmp_path, 2, "cuda", "devloop", round_timeout=6.0, timeout=300,
                         env_extra={"LSD_LOOP_RING_MB": "16", "LSD_TEST_STALL_RANK": "1",
-                                   "LSD_TEST_STALL_AFTER": "25"})
+                                   "LSD_TEST_STALL_AFTER": "8"})
     assert res["err"] is not None and not res["healthy"], res
     assert res["elapsed"] < 6.0 + 30.0, res
