@@ -15,8 +15,7 @@ enum : uint32_t {
 struct LoopChan {
   // written by the sender's kernels only (stream-ordered)
   uint64_t s_seq, s_off;
-  uint32_t s_verdict, r_verdict;  // a wait kernel's outcome for the copy / finish kernels behind it
-  uint64_t r_cur;                 // receiver: ring offset of the message being received
+  uint32_t s_ticket, r_ticket;    // last-block tickets of the op in flight (reset by that block)
   // written by the receiver's release only; polled by the sender
   uint64_t r_seq, r_off;
   // constant after creation

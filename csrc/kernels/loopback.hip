@@ -15,10 +15,8 @@
 //   send  = wait for ring space, copy the payload into the ring, publish the
 //           header {size, offset} and tag = seq + 1
 //   recv  = wait for the tag, check the size, copy out, release the space
-// Up to 128 KiB one block does the whole op (drain + agent-scope release
-// before the tag); above that a 1-block wait, a many-block copy and a 1-block
-// publish / release kernel run in stream order, so kernel boundaries order
-// the payload before its publish and the reads before the release.  Every
+// One launch per op; its last block (agent-scope ticket, every block drained
+// and released first) publishes the tag / releases the space.  Every
 // cross-stream word is an agent-scope atomic (tags / consumed counters),
 // every wait is polled by ONE lane per block, bounded in time (s_memrealtime)
 // and abortable through a word in pinned host memory (the watchdog's abort):
@@ -106,168 +104,110 @@ __device__ __forceinline__ void copy_part(uint8_t* dst, const uint8_t* src, u64 
   }
 }
 
-// No copy kernel ever spins: a wait runs in ONE block (of its own launch for
-// large messages), so however many ops are waiting, they hold a handful of
-// waves -- never the CUs the kernels they wait for need.  (The first version
-// let every block of a 256-block copy spin for ring space; eight stage
-// threads' prefill sends filled the chip with spinning waves and the
-// receives that would free the space could not start: a device-wait timeout
-// in the 8-stage rehearsal, profiles/r4_rehearsal_graph_io.log.)
+// One kernel per op, on at most MAX_BLOCKS blocks: in every block ONE lane
+// polls (bounded) before the block copies its share; the last block to finish
+// (agent-scope ticket) publishes the message / releases its ring space.  The
+// block cap bounds the waves that waiting ops can hold -- MAX_BLOCKS x 4 per
+// op, a few percent of the chip even with every lane of eight stages waiting
+// -- so a waiting op never takes the CUs the kernel it waits for needs.  (The
+// first version spun on up to 256 blocks per op; eight stage threads' prefill
+// sends filled the chip with spinning waves and the receives that would free
+// their ring space could not start: a device-wait timeout in the 8-stage
+// rehearsal.  The second ran wait / copy / finish as three launches, ~6 extra
+// kernels per decode item: profiles/r4_rehearsal_graph_io.log.)
 //
 // `ring` is this process's address of the channel's ring (an IPC mapping when
 // the peer process owns it): pointers never travel through the shared state.
+constexpr int MAX_BLOCKS = 16;
 
 __device__ __forceinline__ bool send_space(const LoopChan* ch, u64 seq, u64 off, u64 bytes) {
   // header slot free and [r_off, off + bytes) within one ring
   return seq - ld_agent(&ch->r_seq) < LOOP_HEADERS && off + bytes - ld_agent(&ch->r_off) <= ch->cap;
 }
 
-// publish message `seq` at `off` (after the payload is visible device-wide)
-__device__ __forceinline__ void publish(LoopChan* ch, u64 seq, u64 off, u64 bytes) {
-  const u32 k = (u32)(seq % LOOP_HEADERS);
-  __hip_atomic_store(&ch->h_size[k], bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&ch->h_off[k], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  st_agent_release(&ch->h_tag[k], seq + 1);
-  ch->s_seq = seq + 1;
-  ch->s_off = off + bytes;
+// The calling block is the last of the launch to get here (ticket), after
+// every block drained its memory operations.  Single lane.
+__device__ __forceinline__ bool last_block(u32* ticket) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this block's stores / completed reads first
+  const u32 t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t != gridDim.x - 1) return false;
+  __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next op
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every other block's release before ours
+  return true;
 }
 
-// wait for message `seq`; 0 and its ring offset in *off, or an error code
-__device__ __forceinline__ u32 recv_head(const LoopChan* ch, u64 seq, u64 bytes, const LoopStatus* st, u64* off) {
-  const u32 k = (u32)(seq % LOOP_HEADERS);
-  u32 v = bounded_wait([&] { return ld_agent(&ch->h_tag[k]) == seq + 1; }, st, ch->spin_limit);
-  if (v) return v;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  *off = ld_agent(&ch->h_off[k]);
-  return ld_agent(&ch->h_size[k]) == bytes ? 0u : (u32)LOOP_ERR_MISMATCH;
-}
-
-__device__ __forceinline__ void release_recv(LoopChan* ch, u64 seq, u64 off, u64 bytes) {
-  st_agent_release(&ch->r_off, off + bytes);
-  st_agent_release(&ch->r_seq, seq + 1);
-}
-
-// --- small messages: one block does wait + copy + publish / release --------
-__global__ __launch_bounds__(THREADS) void loop_send_small(LoopChan* ch, uint8_t* ring, const uint8_t* src,
-                                                           u64 bytes, LoopStatus* st) {
+__global__ __launch_bounds__(THREADS) void loop_send_kernel(LoopChan* ch, uint8_t* ring, const uint8_t* src,
+                                                            u64 bytes, LoopStatus* st) {
   __shared__ u32 verdict;
   const u64 cap = ch->cap, seq = ch->s_seq;  // sender-private: stream-ordered
   const u64 off = place(ch->s_off, bytes, cap);
   if (threadIdx.x == 0) {
-    u32 v = bounded_wait([&] { return send_space(ch, seq, off, bytes); }, st, ch->spin_limit);
+    const u32 v = bounded_wait([&] { return send_space(ch, seq, off, bytes); }, st, ch->spin_limit);
     if (v) set_err(st, v, ch->id);
     verdict = v;
   }
   __syncthreads();
-  if (verdict) return;
+  if (verdict) return;  // the data plane is failed: nothing is published
   copy_part(ring + off % cap, src, bytes);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
   __syncthreads();
-  if (threadIdx.x == 0 && seq < ch->stall_from) {    // stall_from: fault injection
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    publish(ch, seq, off, bytes);
+  if (threadIdx.x == 0 && last_block(&ch->s_ticket) && seq < ch->stall_from) {  // stall_from: tests
+    const u32 k = (u32)(seq % LOOP_HEADERS);
+    __hip_atomic_store(&ch->h_size[k], bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ch->h_off[k], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_agent_release(&ch->h_tag[k], seq + 1);
+    ch->s_seq = seq + 1;  // read by the channel's next send (stream order)
+    ch->s_off = off + bytes;
   }
 }
 
-__global__ __launch_bounds__(THREADS) void loop_recv_small(LoopChan* ch, const uint8_t* ring, uint8_t* dst,
-                                                           u64 bytes, LoopStatus* st) {
+__global__ __launch_bounds__(THREADS) void loop_recv_kernel(LoopChan* ch, const uint8_t* ring, uint8_t* dst,
+                                                            u64 bytes, LoopStatus* st) {
   __shared__ u32 verdict;
   __shared__ u64 s_off;
   const u64 seq = ch->r_seq;  // receiver-private: stream-ordered
   if (threadIdx.x == 0) {
-    u64 off = 0;
-    const u32 v = recv_head(ch, seq, bytes, st, &off);
+    const u32 k = (u32)(seq % LOOP_HEADERS);
+    u32 v = bounded_wait([&] { return ld_agent(&ch->h_tag[k]) == seq + 1; }, st, ch->spin_limit);
+    if (!v) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      s_off = ld_agent(&ch->h_off[k]);
+      if (ld_agent(&ch->h_size[k]) != bytes) v = LOOP_ERR_MISMATCH;
+    }
     if (v) set_err(st, v, ch->id);
     verdict = v;
-    s_off = off;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   if (verdict) return;
-  copy_part(dst, ring + s_off % ch->cap, bytes);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring reads are done
+  const u64 off = s_off;
+  copy_part(dst, ring + off % ch->cap, bytes);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's ring reads are done
   __syncthreads();
-  if (threadIdx.x == 0) release_recv(ch, seq, s_off, bytes);
+  if (threadIdx.x == 0 && last_block(&ch->r_ticket)) {
+    st_agent_release(&ch->r_off, off + bytes);  // the ring space is free again
+    st_agent_release(&ch->r_seq, seq + 1);
+  }
 }
-
-// --- large messages: wait (1 block) / copy (many blocks) / finish (1 block) --
-__global__ void loop_send_wait(LoopChan* ch, u64 bytes, LoopStatus* st) {
-  if (threadIdx.x != 0) return;
-  const u64 seq = ch->s_seq, off = place(ch->s_off, bytes, ch->cap);
-  const u32 v = bounded_wait([&] { return send_space(ch, seq, off, bytes); }, st, ch->spin_limit);
-  if (v) set_err(st, v, ch->id);
-  ch->s_verdict = v;
-}
-
-__global__ __launch_bounds__(THREADS) void loop_send_copy(const LoopChan* ch, uint8_t* ring, const uint8_t* src,
-                                                          u64 bytes) {
-  if (ch->s_verdict) return;
-  copy_part(ring + place(ch->s_off, bytes, ch->cap) % ch->cap, src, bytes);
-}
-
-__global__ void loop_send_publish(LoopChan* ch, u64 bytes) {
-  if (threadIdx.x != 0 || ch->s_verdict) return;
-  const u64 seq = ch->s_seq;
-  if (seq >= ch->stall_from) return;  // fault injection: the peer waits on the device
-  // the payload (previous kernel) is visible: kernel boundary
-  publish(ch, seq, place(ch->s_off, bytes, ch->cap), bytes);
-}
-
-__global__ void loop_recv_wait(LoopChan* ch, u64 bytes, LoopStatus* st) {
-  if (threadIdx.x != 0) return;
-  u64 off = 0;
-  const u32 v = recv_head(ch, ch->r_seq, bytes, st, &off);
-  if (v) set_err(st, v, ch->id);
-  ch->r_verdict = v;
-  ch->r_cur = off;
-}
-
-__global__ __launch_bounds__(THREADS) void loop_recv_copy(const LoopChan* ch, const uint8_t* ring, uint8_t* dst,
-                                                          u64 bytes) {
-  if (ch->r_verdict) return;
-  copy_part(dst, ring + ch->r_cur % ch->cap, bytes);
-}
-
-__global__ void loop_recv_release(LoopChan* ch, u64 bytes) {
-  if (threadIdx.x != 0 || ch->r_verdict) return;
-  // the copy kernel's reads of the ring completed before this kernel began
-  release_recv(ch, ch->r_seq, ch->r_cur, bytes);
-}
-
-constexpr u64 SMALL = 128 << 10;  // one-block ops up to this many bytes
 
 int copy_blocks(u64 bytes) {
   const u64 b = (bytes + CHUNK - 1) / CHUNK;
-  return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
+  return (int)(b < 1 ? 1 : (b > MAX_BLOCKS ? MAX_BLOCKS : b));
 }
 
 }  // namespace
 
 extern "C" hipError_t lsd_loop_send(LoopChan* ch, void* ring, const void* src, uint64_t bytes,
                                     LoopStatus* st, hipStream_t s) {
-  auto* r = static_cast<uint8_t*>(ring);
-  auto* p = static_cast<const uint8_t*>(src);
-  if (bytes <= SMALL) {
-    hipLaunchKernelGGL(loop_send_small, dim3(1), dim3(THREADS), 0, s, ch, r, p, bytes, st);
-  } else {
-    hipLaunchKernelGGL(loop_send_wait, dim3(1), dim3(64), 0, s, ch, bytes, st);
-    hipLaunchKernelGGL(loop_send_copy, dim3(copy_blocks(bytes)), dim3(THREADS), 0, s, ch, r, p, bytes);
-    hipLaunchKernelGGL(loop_send_publish, dim3(1), dim3(64), 0, s, ch, bytes);
-  }
+  hipLaunchKernelGGL(loop_send_kernel, dim3(copy_blocks(bytes)), dim3(THREADS), 0, s, ch,
+                     static_cast<uint8_t*>(ring), static_cast<const uint8_t*>(src), bytes, st);
   return hipGetLastError();
 }
 
 extern "C" hipError_t lsd_loop_recv(LoopChan* ch, const void* ring, void* dst, uint64_t bytes,
                                     LoopStatus* st, hipStream_t s) {
-  auto* r = static_cast<const uint8_t*>(ring);
-  auto* p = static_cast<uint8_t*>(dst);
-  if (bytes <= SMALL) {
-    hipLaunchKernelGGL(loop_recv_small, dim3(1), dim3(THREADS), 0, s, ch, r, p, bytes, st);
-  } else {
-    hipLaunchKernelGGL(loop_recv_wait, dim3(1), dim3(64), 0, s, ch, bytes, st);
-    hipLaunchKernelGGL(loop_recv_copy, dim3(copy_blocks(bytes)), dim3(THREADS), 0, s, ch, r, p, bytes);
-    hipLaunchKernelGGL(loop_recv_release, dim3(1), dim3(64), 0, s, ch, bytes);
-  }
+  hipLaunchKernelGGL(loop_recv_kernel, dim3(copy_blocks(bytes)), dim3(THREADS), 0, s, ch,
+                     static_cast<const uint8_t*>(ring), static_cast<uint8_t*>(dst), bytes, st);
   return hipGetLastError();
 }
 
