@@ -154,7 +154,10 @@ void wait_ops(Fabric* f, const Ops& ops) {
       if (ok) break;
       if (f->aborted.load(std::memory_order_relaxed))
         throw std::runtime_error(chan_name(c) + ": data plane aborted");
-      if (spins < 2000) {
+      // a short yield spin (the peer is usually microseconds away), then
+      // sleeps: up to 8 stage threads wait at once, and yield-spinning ones
+      // take the host CPUs that the threads they wait for need
+      if (spins < 64) {
         std::this_thread::yield();
         continue;
       }
@@ -162,7 +165,7 @@ void wait_ops(Fabric* f, const Ops& ops) {
         throw std::runtime_error(chan_name(c) + ": timed out waiting for the peer stage (" +
                                  std::string(op.dir ? "receive: no matching send" : "send: ring full") +
                                  ")");
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      std::this_thread::sleep_for(std::chrono::microseconds(spins < 256 ? 5 : 25));
     }
   }
 }
