@@ -274,11 +274,15 @@ class Engine(racecheck.Shared):
     def _devloop_fabric(self, dev: torch.device) -> DeviceLoopFabric:
         """Loopback channels sized for the largest message an edge carries:
         one item's prefill rows (a group's chunk tokens, fp32) or decode rows;
-        two of them fit each ring.  LSD_LOOP_RING_MB overrides."""
+        eight of them fit each ring (64 MiB - 1 GiB) -- with two, the prefill
+        senders of an 8-stage rehearsal waited for ring space (GPT-2 small P=8:
+        287k -> 300k tok/s with 512 MiB rings, profiles/r4_ab_rehearsal.log).
+        LSD_LOOP_RING_MB overrides."""
         cfg, H = self.cfg, self.mcfg.hidden
         per_seq = cfg.prefill_chunk if cfg.prefill_chunk > 0 else self.max_seq
         big = self.group_cap * min(per_seq, self.max_seq) * H * 4
-        ring = int(os.environ.get("LSD_LOOP_RING_MB", "0")) << 20 or max(8 << 20, 2 * big + (1 << 20))
+        ring = int(os.environ.get("LSD_LOOP_RING_MB", "0")) << 20 or min(1 << 30, max(64 << 20, 8 * big))
+        ring = max(ring, big + (1 << 20))
         return DeviceLoopFabric(self.P, dev, lanes=int(os.environ.get("LSD_LANES", "2")), ring_bytes=ring,
                                 timeout=cfg.round_timeout_s,
                                 spin_limit_s=float(os.environ.get("LSD_LOOP_SPIN_S", "30")))
