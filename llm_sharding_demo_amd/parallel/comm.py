@@ -139,6 +139,9 @@ class _DistTransport(Transport):
         # inherit the default group's timeout: gloo would wait 30 min on a
         # dead peer)
         kw = {"timeout": datetime.timedelta(seconds=timeout_s)} if timeout_s else {}
+        # the control group carries bring-up collectives (communicator ids,
+        # warm-up barriers, KV sizing) and stats: never shorter than 10 min
+        ckw = {"timeout": datetime.timedelta(seconds=max(timeout_s, 600.0))} if timeout_s else {}
         self.groups: Dict[str, object] = {}
         for rep in range(R):
             base = rep * P
@@ -148,7 +151,7 @@ class _DistTransport(Transport):
             if P > 1:
                 self.groups[f"r{rep}ret"] = (dist.new_group([base + P - 1, base], backend=self._backend(), **kw)
                                              if self.EDGE_GROUPS else None)
-        self.ctrl = dist.new_group(list(range(P * R)), backend="gloo", **kw)
+        self.ctrl = dist.new_group(list(range(P * R)), backend="gloo", **ckw)
         # step plans (rank 0 -> every rank) and DP token readouts (replica
         # stage 0 -> rank 0) travel on their own gloo groups with no practical
         # timeout: an idle server waits on them indefinitely

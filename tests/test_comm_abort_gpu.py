@@ -32,6 +32,7 @@ def _transport_with(C, h):
     # replica 0, stage 0; the forward edge's communicator is the 1-rank one,
     # registered as member 1 so that its peer (1 - me) is rank 0 = itself
     t.C, t.L, t.aborted, t._lock = C, 1, False, threading.Lock()
+    t._issue, t._inflight = threading.Condition(), 0  # the abort gate (advisor r3)
     t.replica, t.rank = 0, 0
     t.comms = {("r0fwd0", 0): (h, 1)}
     return t

@@ -64,9 +64,10 @@ def _run(tmp_path, world, device, transport, dp=1, greedy=True, env_extra=None, 
                     eng.worker_loop()
                 finally:
                     w = eng.workers[0]
-                    print("EVID", json.dumps(dict(rank=eng.rank, native=w.native_steps, io=w.io_items,
-                                                  graph_io=w.graph_io, comms=eng.transport.num_comms)),
-                          flush=True)
+                    # one write per line: ranks share the pipe, print() writes text and newline separately
+                    os.write(1, ("EVID " + json.dumps(dict(rank=eng.rank, native=w.native_steps, io=w.io_items,
+                                                            graph_io=w.graph_io, comms=eng.transport.num_comms))
+                                 + "\\n").encode())
             else:
                 t0 = time.monotonic()
                 err = None
@@ -77,10 +78,10 @@ def _run(tmp_path, world, device, transport, dp=1, greedy=True, env_extra=None, 
                     out = out2 = None
                     err = f"{{type(e).__name__}}: {{e}}"
                 w = eng.workers[0]
-                print("RESULT", json.dumps(dict(out=out, out2=out2, err=err, healthy=eng.healthy,
-                                                elapsed=time.monotonic() - t0, native=w.native_steps,
-                                                graph_io=w.graph_io, world=eng.transport.gworld,
-                                                comms=eng.transport.num_comms)), flush=True)
+                os.write(1, ("RESULT " + json.dumps(dict(out=out, out2=out2, err=err, healthy=eng.healthy,
+                                                          elapsed=time.monotonic() - t0, native=w.native_steps,
+                                                          graph_io=w.graph_io, world=eng.transport.gworld,
+                                                          comms=eng.transport.num_comms)) + "\\n").encode())
                 if err is None:
                     eng.shutdown()
         except Exception as e:
@@ -95,9 +96,11 @@ def _run(tmp_path, world, device, transport, dp=1, greedy=True, env_extra=None, 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={port}", str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
-    res = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+    res = [l[l.index("RESULT"):] for l in r.stdout.splitlines() if "RESULT {" in l]
     assert res, (r.returncode, r.stdout[-3000:], r.stderr[-5000:])
-    evid = [json.loads(l[5:]) for l in r.stdout.splitlines() if l.startswith("EVID ")]
+    import re
+
+    evid = [json.loads(m) for m in re.findall(r"EVID (\{[^{}]*\})", r.stdout)]
     return json.loads(res[0][len("RESULT "):]), evid, r
 
 
