@@ -142,6 +142,11 @@ class _DistTransport(Transport):
         # the control group carries bring-up collectives (communicator ids,
         # warm-up barriers, KV sizing) and stats: never shorter than 10 min
         ckw = {"timeout": datetime.timedelta(seconds=max(timeout_s, 600.0))} if timeout_s else {}
+        self.ctrl = dist.new_group(list(range(P * R)), backend="gloo", **ckw)
+        # every rank reaches the edge groups' connect phase together: a rank
+        # still importing / binding its GPU must not exhaust a short round
+        # deadline there (seen with a 4 s deadline on a loaded host)
+        dist.barrier(group=self.ctrl)
         self.groups: Dict[str, object] = {}
         for rep in range(R):
             base = rep * P
@@ -151,7 +156,6 @@ class _DistTransport(Transport):
             if P > 1:
                 self.groups[f"r{rep}ret"] = (dist.new_group([base + P - 1, base], backend=self._backend(), **kw)
                                              if self.EDGE_GROUPS else None)
-        self.ctrl = dist.new_group(list(range(P * R)), backend="gloo", **ckw)
         # step plans (rank 0 -> every rank) and DP token readouts (replica
         # stage 0 -> rank 0) travel on their own gloo groups with no practical
         # timeout: an idle server waits on them indefinitely
@@ -1213,7 +1217,9 @@ def init_distributed(backend: str, device_type: str, timeout_s: float = 600.0) -
     if dist.is_initialized():
         return
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-    kw = {"timeout": datetime.timedelta(seconds=timeout_s)}
+    # the default group only carries bring-up (rendezvous, group creation):
+    # never shorter than 10 min; data-plane groups get the round deadline
+    kw = {"timeout": datetime.timedelta(seconds=max(timeout_s, 600.0))}
     if device_type == "cuda":
         # one rank per GPU; more ranks than GPUs (single-GPU rehearsal over
         # gloo) wrap around.  device_count() does not initialise HIP.
