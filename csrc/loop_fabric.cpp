@@ -387,10 +387,13 @@ void lsd_register_loopback(py::module& m) {
   m.def("loop_shm_map", [](const std::string& name, int64_t bytes, bool create) {
     int fd = shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
     if (fd < 0) throw std::runtime_error("shm_open(" + name + "): " + std::strerror(errno));
-    if (create && ftruncate(fd, (off_t)bytes) != 0) {
-      close(fd);
-      shm_unlink(name.c_str());
-      throw std::runtime_error("ftruncate(" + name + "): " + std::strerror(errno));
+    if (create) {  // pages reserved now (no SIGBUS later on a full /dev/shm)
+      const int rc = ftruncate(fd, (off_t)bytes) != 0 ? errno : posix_fallocate(fd, 0, (off_t)bytes);
+      if (rc != 0) {
+        close(fd);
+        shm_unlink(name.c_str());
+        throw std::runtime_error("reserving shared memory " + name + ": " + std::strerror(rc));
+      }
     }
     void* p = mmap(nullptr, (size_t)bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);

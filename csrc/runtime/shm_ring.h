@@ -45,10 +45,15 @@ class ShmRing {
     const size_t bytes = sizeof(Header) + (size_t)slots * slot_bytes;
     int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd < 0) throw std::runtime_error("shm_open(create " + name + "): " + std::strerror(errno));
-    if (ftruncate(fd, (off_t)bytes) != 0) {
+    // reserve every page now: a sparse tmpfs file that later outgrows
+    // /dev/shm (64 MiB in a default container) faults the writer with SIGBUS
+    // mid-run; a reservation that does not fit fails here, and the caller
+    // falls back to the gloo plan records
+    int rc = ftruncate(fd, (off_t)bytes) != 0 ? errno : posix_fallocate(fd, 0, (off_t)bytes);
+    if (rc != 0) {
       close(fd);
       shm_unlink(name.c_str());
-      throw std::runtime_error("ftruncate(" + name + "): " + std::strerror(errno));
+      throw std::runtime_error("reserving " + std::to_string(bytes) + " B for " + name + ": " + std::strerror(rc));
     }
     auto* r = new ShmRing(name, fd, bytes, -1);
     Header* h = r->hdr_;

@@ -571,8 +571,10 @@ class ShmPlanChannel:
 
     INLINE, VIA_GLOO = b"I", b"G"
 
+    # 64 x 256 KiB = 16 MiB of /dev/shm per replica, reserved up front; a
+    # pickled plan too large for a slot travels over gloo behind its record
     def __init__(self, transport: "_DistTransport", timeout_s: float, slots: int = 64,
-                 slot_bytes: int = 4 << 20):
+                 slot_bytes: int = 256 << 10):
         import secrets
 
         from ..runtime import native
