@@ -14,9 +14,9 @@ run() {  # label, env...
   grep "^{" gpurun_out/_r.out >> $L
 }
 run "default" LSD_X=0 && \
-run "RESID_TARGET=50 (1 split)" LSD_RING_RESID_TARGET=50 && \
-run "RESID_TARGET=100 (2 splits)" LSD_RING_RESID_TARGET=100 && \
-run "RESID_TARGET=150 (3 splits)" LSD_RING_RESID_TARGET=150 && \
+run "RESID_TARGET=300 (3 / 6 splits)" LSD_RING_RESID_TARGET=300 && \
+run "RESID_TARGET=350 (3 / 7 splits)" LSD_RING_RESID_TARGET=350 && \
+run "RESID_TARGET=450 (3 / 9 splits)" LSD_RING_RESID_TARGET=450 && \
 run "default (again)" LSD_X=0
 rc=$?
 python3 - <<'PY'
