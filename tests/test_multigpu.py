@@ -170,7 +170,7 @@ def test_rccl_stall_abort_unblocks_recv(tmp_path):
 # ---------------------------------------------------------------------------
 # CPU twins: the same worker script over gloo
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("world,dp,chunk", [(2, 1, 0), (4, 1, 2), (4, 2, 0)])
+@pytest.mark.parametrize("world,dp,chunk", [(2, 1, 0), (4, 1, 2), (4, 2, 0), (8, 1, 2), (8, 2, 0)])
 def test_gloo_twin_matches_one_stage(tmp_path, world, dp, chunk):
     res, evid, r = _run(tmp_path, world, "cpu", "gloo", dp=dp, greedy=False, chunk=chunk, timeout=300)
     assert res["err"] is None, (res, r.stderr[-4000:])
