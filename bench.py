@@ -215,6 +215,11 @@ def main() -> int:
                        "sampler": "greedy" if args.greedy else "T0.6/top-k40",
                        "hipgraphs": not args.no_graphs},
         }
+        C = getattr(getattr(eng.stages[0], "backend", None), "C", None) if eng.stages else None
+        if C is not None and hasattr(C, "gemm_slab_bf16"):
+            # precision of the residual projections' split-K partials (bf16 = one
+            # rounding per partial before the fp32 residual add; LSD_SLAB_BF16=0: fp32)
+            out["split_k_slabs"] = "bf16" if C.gemm_slab_bf16() else "fp32"
         if (args.loopback_stages or N > 1) and eng.last_session is not None:
             out["stage_busy"] = [st["busy_fraction"] for st in eng.last_session.stages]
         if N > 1 or args.loopback_stages:

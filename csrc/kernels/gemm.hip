@@ -48,6 +48,13 @@ template <int EPI>
 __device__ __forceinline__ void epilogue4(const GemmParams& p, int row0, int n, f32x4 v, f32x4 v2,
                                           int split) {
   if constexpr (EPI == EPI_SLAB) {
+    if (p.slab_bf16) {
+      bf16* s = reinterpret_cast<bf16*>(p.slab) + (long)split * p.M * p.N;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (row0 + i < p.M) s[(long)(row0 + i) * p.N + n] = f2bf(v[i]);
+      return;
+    }
     float* s = p.slab + (long)split * p.M * p.N;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -175,6 +182,15 @@ __device__ __forceinline__ void epi8_pre2(const GemmParams& p, int n, Epi8Pre& e
 template <int EPI>
 __device__ __forceinline__ void epi8_post(const GemmParams& p, int m, int n, const float* v, int split,
                                           const Epi8Pre& e) {
+  if constexpr (EPI == EPI_SLAB) {
+    if (p.slab_bf16) {  // half the slab bytes for the GEMM to write and the norm to read
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+      st8(reinterpret_cast<bf16*>(p.slab) + (long)split * p.M * p.N + (long)m * p.N + n, o);
+      return;
+    }
+  }
   if constexpr (EPI == EPI_SLAB || EPI == EPI_F32) {
     float* o = EPI == EPI_SLAB ? p.slab + (long)split * p.M * p.N + (long)m * p.N + n
                                : reinterpret_cast<float*>(p.out) + (long)m * p.ldo + n;

@@ -23,6 +23,7 @@ struct GemmParams {
   int q_size, kv_size, hd, max_seq, n_kv;
   const float* rope;  // [max_pos][hd/2][2] (cos, sin), or null
   long long* stamps;  // diagnostic builds only: per-workgroup s_memrealtime phase stamps
+  int slab_bf16;      // EPI_SLAB: partial slabs stored bf16 instead of fp32 (LSD_SLAB_BF16)
 };
 
 // Small-M (M <= 8) weight-streaming GEMV with an optional fused input norm

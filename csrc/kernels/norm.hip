@@ -45,13 +45,25 @@ __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids,
 // SPL >= 0: exactly SPL split-K slabs, every slab load of the row issued
 // before the first add (one memory round trip instead of one per slab: the
 // runtime-count loop serialised them, ~1 us each); SPL < 0: runtime count.
-template <int MAXV, bool RMS, int SPL>
-__global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __restrict__ slab,
+// SB: the slabs are bf16 (LSD_SLAB_BF16: half the bytes), else fp32.
+template <int MAXV, bool RMS, int SPL, bool SB = false>
+__global__ __launch_bounds__(256) void norm_kernel(float* x, const void* __restrict__ slab_,
                                                    int splits, const bf16* __restrict__ pbias,
                                                    const bf16* __restrict__ w,
                                                    const bf16* __restrict__ b, bf16* out, int T,
                                                    int H, float eps, const int* __restrict__ rows) {
   __shared__ float red[24];
+  const float* slab = static_cast<const float*>(slab_);
+  const bf16* slab_h = static_cast<const bf16*>(slab_);
+  // one slab element group of 4 at (split s, row, column c)
+  auto slab4 = [&](int s, int row, int c) -> f32x4 {
+    if constexpr (SB) {
+      const bf16x4 h = ld4(slab_h + ((long)s * T + row) * H + c);
+      return f32x4{bf2f(h[0]), bf2f(h[1]), bf2f(h[2]), bf2f(h[3])};
+    } else {
+      return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(slab + ((long)s * T + row) * H + c));
+    }
+  };
   const int t = blockIdx.x;
   // gamma / beta are issued first: their latency overlaps the row loads
   // instead of adding a second memory round trip after the reductions
@@ -82,9 +94,7 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __rest
       xa[g] = *reinterpret_cast<const f32x4*>(xr + cc);
       if (slab && pbias) pbv[g] = ld4(pbias + cc);
 #pragma unroll
-      for (int s = 0; s < NL; ++s)
-        part[g][s] = __builtin_nontemporal_load(
-            reinterpret_cast<const f32x4*>(slab + ((long)s * T + src) * H + cc));
+      for (int s = 0; s < NL; ++s) part[g][s] = slab4(s, src, cc);
     }
 #pragma unroll
     for (int g = 0; g < GRP; ++g) {
@@ -95,8 +105,7 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const float* __rest
 #pragma unroll
         for (int s = 0; s < NL; ++s) a += part[g][s];
         if (SPL < 0 && slab)
-          for (int s = 0; s < splits; ++s)
-            a += *reinterpret_cast<const f32x4*>(slab + ((long)s * T + src) * H + c);
+          for (int s = 0; s < splits; ++s) a += slab4(s, src, c);
         if (slab) {
           if (pbias) {
             const bf16x4 pb = pbv[g];
@@ -165,19 +174,25 @@ extern "C" hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte,
   return hipGetLastError();
 }
 
-extern "C" hipError_t lsd_norm(float* x, const float* slab, int splits, const bf16* pbias,
+extern "C" hipError_t lsd_norm(float* x, const void* slab, int slab_bf16, int splits, const bf16* pbias,
                                const bf16* w, const bf16* b, bf16* out, int T, int H, float eps,
                                int rms, const int* rows, int nrows, hipStream_t st) {
   const int n = rows ? nrows : T;
   if (n == 0) return hipSuccess;
   const int maxv = (H + 1023) / 1024;
-#define LSD_NORM_S(MV, S)                                                                     \
-  if (rms)                                                                                    \
-    hipLaunchKernelGGL((norm_kernel<MV, true, S>), dim3(n), dim3(256), 0, st, x, slab, splits, \
-                       pbias, w, b, out, T, H, eps, rows);                                    \
-  else                                                                                        \
-    hipLaunchKernelGGL((norm_kernel<MV, false, S>), dim3(n), dim3(256), 0, st, x, slab,      \
+#define LSD_NORM_T(MV, S, SB)                                                                     \
+  if (rms)                                                                                        \
+    hipLaunchKernelGGL((norm_kernel<MV, true, S, SB>), dim3(n), dim3(256), 0, st, x, slab, splits, \
+                       pbias, w, b, out, T, H, eps, rows);                                        \
+  else                                                                                            \
+    hipLaunchKernelGGL((norm_kernel<MV, false, S, SB>), dim3(n), dim3(256), 0, st, x, slab,      \
                        splits, pbias, w, b, out, T, H, eps, rows);
+#define LSD_NORM_S(MV, S)      \
+  if (slab_bf16 && slab) {     \
+    LSD_NORM_T(MV, S, true)    \
+  } else {                     \
+    LSD_NORM_T(MV, S, false)   \
+  }
 #define LSD_NORM(MV)                   \
   switch (slab ? splits : 0) {         \
     case 0: LSD_NORM_S(MV, 0) break;   \
@@ -200,6 +215,7 @@ extern "C" hipError_t lsd_norm(float* x, const float* slab, int splits, const bf
   } else {
     return hipErrorInvalidValue;
   }
+#undef LSD_NORM_T
 #undef LSD_NORM_S
 #undef LSD_NORM
   return hipGetLastError();

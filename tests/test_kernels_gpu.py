@@ -41,13 +41,14 @@ def test_embed(C):
 @pytest.mark.parametrize("H", [128, 768, 1600, 4096, 8192])
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("S", [1, 3, 8, 12])  # exact-count unrolled slabs (<= 8) and runtime loop
-def test_norm_with_slab_combine(C, H, rms, S):
+@pytest.mark.parametrize("sdt", [torch.float32, torch.bfloat16])  # LSD_SLAB_BF16 slabs
+def test_norm_with_slab_combine(C, H, rms, S, sdt):
     T = 19
     x = torch.randn(T, H, device=DEV)
-    slab = torch.randn(S, T, H, device=DEV) * 0.1
+    slab = (torch.randn(S, T, H, device=DEV) * 0.1).to(sdt)
     pb = bf(H, scale=0.1, seed=3)
     w, b = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16(), bf(H, scale=0.1, seed=4)
-    x_ref = x + slab.sum(0) + pb.float()
+    x_ref = x + slab.float().sum(0) + pb.float()
     y_ref = ref.rmsnorm(x_ref, w, 1e-5) if rms else ref.layernorm(x_ref, w, b, 1e-5)
     y = C.norm(x, slab, pb, w, None if rms else b, 1e-5, rms, None, True)
     close(x, x_ref, 1e-5)
@@ -60,6 +61,35 @@ def test_norm_with_slab_combine(C, H, rms, S):
 @pytest.fixture(scope="module")
 def CNT():
     return torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
+
+
+@pytest.fixture(autouse=True)
+def _fp32_slabs(C):
+    """The GEMM tests below check split-K residual slabs at fp32 precision; the
+    bf16 slabs of production decode (LSD_SLAB_BF16) have their own test."""
+    prev = C.gemm_slab_bf16()
+    C.gemm_set_slab_bf16(0)
+    yield
+    C.gemm_set_slab_bf16(int(prev))
+
+
+@pytest.mark.parametrize("tiled,M,splits", [(True, 256, 3), (True, 256, 5), (True, 130, 3), (False, 64, 5)])
+def test_linear_residual_bf16_slabs(C, CNT, tiled, M, splits):
+    """bf16 partial slabs: each split's partial rounded once to bf16 (a bf16
+    GEMM output's precision), folded into the fp32 residual by the norm."""
+    C.gemm_set_slab_bf16(1)
+    N, K = 1600, 1600
+    a, w, bias = bf(M, K, seed=8), bf(N, K, scale=0.05, seed=9), bf(N, scale=0.1, seed=10)
+    x = torch.randn(M, N, device=DEV)
+    y = ref.linear(a, w, bias)
+    x_ref = x + y
+    slab = C.linear_residual(a, w, bias, x, splits, tiled, CNT, not tiled)
+    assert slab is not None and slab.dtype == torch.bfloat16 and slab.shape == (splits, M, N)
+    C.norm(x, slab, bias, None, None, 0.0, True, None, False)
+    # error of S bf16 roundings of partials of |y| / sqrt(S)-ish size
+    err = (x - x_ref).abs()
+    assert float(err.max()) <= 2.0 ** -8 * float(y.abs().max()) * splits, float(err.max())
+    assert float(err.mean()) <= 2.0 ** -9 * float(y.abs().mean()) * 2, float(err.mean())
 
 
 @pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 65, 100, 128, 200])

@@ -97,7 +97,10 @@ def _run(tmp_path, world, device, transport, dp=1, greedy=True, env_extra=None, 
            "--master-addr=127.0.0.1", f"--master-port={port}", str(script)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     res = [l[l.index("RESULT"):] for l in r.stdout.splitlines() if "RESULT {" in l]
-    assert res, (r.returncode, r.stdout[-3000:], r.stderr[-5000:])
+    if not res:  # keep the lines that say what went wrong (the tail is mostly torchrun's summary)
+        keep = [l for l in (r.stdout + r.stderr).splitlines()
+                if any(k in l for k in ("FAIL", "Error", "error", "Traceback", "line ", "raise"))]
+        raise AssertionError(f"rc {r.returncode}\n" + "\n".join(keep[-60:]))
     import re
 
     evid = [json.loads(m) for m in re.findall(r"EVID (\{[^{}]*\})", r.stdout)]
