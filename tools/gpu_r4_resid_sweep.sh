@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: residual-projection K splits at 256 rows (LSD_RING_RESID_TARGET: workgroup target of the
+# Round 4: residual-projection K splits (bf16 slabs: the default since the slab A/B) at 256 rows (LSD_RING_RESID_TARGET: workgroup target of the
 # split-K residual GEMMs on the 8-wave ring; 256 default = 3 / 5 splits for GPT-2 XL's K 1600 / 6400).
 # Fewer splits = fewer slabs for the next norm to fold and fewer workgroups beside the other lane's
 # attention.  Headline config, same box, default run first and last.
@@ -14,6 +14,7 @@ run() {  # label, env...
   grep "^{" gpurun_out/_r.out >> $L
 }
 run "default" LSD_X=0 && \
+run "RESID_TARGET=200 (3 / 4 splits)" LSD_RING_RESID_TARGET=200 && \
 run "RESID_TARGET=300 (3 / 6 splits)" LSD_RING_RESID_TARGET=300 && \
 run "RESID_TARGET=350 (3 / 7 splits)" LSD_RING_RESID_TARGET=350 && \
 run "RESID_TARGET=450 (3 / 9 splits)" LSD_RING_RESID_TARGET=450 && \
