@@ -225,6 +225,9 @@ class HipBackend(Backend):
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))
+        lw = int(os.environ.get("LSD_ATTN_LARGE_WAVES", "4"))  # full-batch decode attention block (4 / 8 waves)
+        self.C.attn_set_large_waves(64, lw)
+        self.C.attn_set_large_waves(128, lw)
         self.counters = None
         self._rope = None
         self.lane = 0  # microbatch lane (stream) currently being issued; see pipeline.py
