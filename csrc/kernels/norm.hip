@@ -58,7 +58,10 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const void* __restr
   // one slab element group of 4 at (split s, row, column c)
   auto slab4 = [&](int s, int row, int c) -> f32x4 {
     if constexpr (SB) {
-      const bf16x4 h = ld4(slab_h + ((long)s * T + row) * H + c);
+      // read-once slabs: non-temporal loads (+0.6-1.3 % on the headline
+      // over default-policy loads, profiles/r4_slab_bf16.log)
+      const bf16x4 h = __builtin_bit_cast(
+          bf16x4, __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(slab_h + ((long)s * T + row) * H + c)));
       return f32x4{bf2f(h[0]), bf2f(h[1]), bf2f(h[2]), bf2f(h[3])};
     } else {
       return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(slab + ((long)s * T + row) * H + c));
