@@ -73,7 +73,10 @@ def _fp32_slabs(C):
     C.gemm_set_slab_bf16(int(prev))
 
 
-@pytest.mark.parametrize("tiled,M,splits", [(True, 256, 3), (True, 256, 5), (True, 130, 3), (False, 64, 5)])
+# 8-wave decode ring (256 / 130 rows), split-K decode kernel (64 rows, deferred) and the
+# 256x256 prefill-class kernel (1024 rows x 6 splits = 168 tiles)
+@pytest.mark.parametrize("tiled,M,splits", [(True, 256, 3), (True, 256, 5), (True, 130, 3), (False, 64, 5),
+                                            (True, 1024, 6)])
 def test_linear_residual_bf16_slabs(C, CNT, tiled, M, splits):
     """bf16 partial slabs: each split's partial rounded once to bf16 (a bf16
     GEMM output's precision), folded into the fp32 residual by the norm."""
