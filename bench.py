@@ -146,11 +146,13 @@ def main() -> int:
         if args.device != "cpu":
             torch.cuda.synchronize()
 
+    last_out = [None]
+
     def session(timing: bool):
         """One bench step = one generation session of the whole global batch:
         every sequence joins at step 0 (prefill), decodes, and leaves."""
         if rank == 0:
-            eng.generate_ids(prompts, [sp] * B, record_timing=timing)
+            last_out[0] = eng.generate_ids(prompts, [sp] * B, record_timing=timing)
         else:
             eng.follow_session()
 
@@ -228,6 +230,14 @@ def main() -> int:
             out["pg_world_size"] = ranks[0]["pg_world"]
             out["data_plane_comms"] = sum(r["comms"] for r in ranks)
             out["rank_devices"] = [r["device"] for r in ranks]
+        rc = 0
+        if N > 1 and os.environ.get("BENCH_CHECK", "1") != "0":
+            # outside the timed region: the pipeline's tokens of the last timed
+            # session against a 1-stage engine on this rank's own GPU
+            chk = check_against_one_gpu(cfg, eng, prompts, sp, last_out[0])
+            out.update(chk)
+            if not chk["pipeline_matches_1gpu"]:
+                rc = 3
         print(json.dumps(out), flush=True)
         hp = getattr(eng, "_hostprof", None)
         if hp is not None and hp[3]:
@@ -241,7 +251,46 @@ def main() -> int:
             eng.shutdown()  # stop the followers, barrier, tear the groups down in order
         else:
             eng.worker_loop()
-    return 0
+    return rc if rank == 0 else 0
+
+
+def check_against_one_gpu(cfg, eng, prompts, sp, got) -> dict:
+    """Token-for-token check of a multi-rank run (rank 0, after the timed
+    region): the first BENCH_CHECK_SEQS (default 512) sequences of replica 0
+    -- whole microbatch groups, in the scheduler's admission order -- are
+    generated again by a 1-stage engine on rank 0's own device with the same
+    weights (seeded per layer), group rows, prefill chunking and sampling
+    (seeded counter-based draws keyed by (seed, step), not by slot or rank).
+    The same GEMM shapes per group and an fp32 residual on the wire make the
+    pipeline bit-identical to one stage, so any difference is a data-plane
+    fault.  This replaces the reference's relay (`/root/reference/server.py:171-181`),
+    which nothing checks either."""
+    import dataclasses
+
+    from llm_sharding_demo_amd.runtime.engine import Engine
+
+    rows = eng.group_cap
+    want_seqs = int(os.environ.get("BENCH_CHECK_SEQS", "512"))
+    groups = max(1, min(eng.M, want_seqs // rows))
+    n = min(groups * rows, len(prompts), len(got))
+    t0 = time.perf_counter()
+    ref_cfg = dataclasses.replace(cfg, num_stages=1, dp_replicas=1, max_batch=groups * rows,
+                                  num_microbatches=groups, transport="auto",
+                                  device=str(eng.devices[0]))
+    ref = Engine(ref_cfg, mode="local")
+    try:
+        want = ref.generate_ids(prompts[:n], [sp] * n)
+    finally:
+        ref.shutdown()
+    bad = [i for i in range(n) if want[i] != got[i]]
+    res = {"pipeline_matches_1gpu": not bad, "check_seqs": n, "check_groups": groups,
+           "check_s": round(time.perf_counter() - t0, 2)}
+    if bad:
+        res["check_mismatched_seqs"] = len(bad)
+        print(f"pipeline/1-GPU token mismatch in {len(bad)} of {n} sequences (first: {bad[0]})",
+              file=sys.stderr, flush=True)
+    del ref
+    return res
 
 
 if __name__ == "__main__":

@@ -150,6 +150,8 @@ PYBIND11_MODULE(_runtime, m) {
            }, py::arg("timeout_s"))
       .def("unlink", &ShmRing::unlink)
       .def("close", &ShmRing::close_ring)
+      .def_property_readonly("closed", &ShmRing::closed)
+      .def("producer_alive", &ShmRing::producer_alive)
       .def_property_readonly("head", &ShmRing::head)
       .def("cursor", &ShmRing::cursor)
       .def_property_readonly("slots", &ShmRing::slots)

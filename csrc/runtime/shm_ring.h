@@ -16,8 +16,14 @@
 // (no overwrite of unread data), then release-stores head = k + 1; reader i
 // acquire-loads head, copies the slot and release-stores cursor[i] = k + 1.
 // Waits spin briefly, then sleep with backoff, and give up at their timeout.
+// The producer stores its pid in the header: a reader whose wait times out can
+// tell a quiet producer from a dead one (producer_alive), and close_ring()
+// ends every reader's wait once the ring is drained.
 #pragma once
 
+#include <signal.h>
+
+#include <cerrno>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -62,9 +68,10 @@ class ShmRing {
     h->readers = (uint32_t)readers;
     h->head.store(0, std::memory_order_relaxed);
     h->closed.store(0, std::memory_order_relaxed);
+    h->producer_pid.store((int64_t)getpid(), std::memory_order_relaxed);
     for (int i = 0; i < kMaxReaders; ++i) h->cursor[i].v.store(0, std::memory_order_relaxed);
-    std::atomic_thread_fence(std::memory_order_release);
-    h->magic = kMagic;
+    // publishes the geometry above: attach() acquire-loads the magic first
+    h->magic.store(kMagic, std::memory_order_release);
     return r;
   }
 
@@ -78,7 +85,8 @@ class ShmRing {
       throw std::runtime_error("fstat(" + name + ")");
     }
     auto* r = new ShmRing(name, fd, (size_t)st.st_size, index);
-    if (r->hdr_->magic != kMagic || index < 0 || index >= (int)r->hdr_->readers) {
+    if ((size_t)st.st_size < sizeof(Header) || r->hdr_->magic.load(std::memory_order_acquire) != kMagic ||
+        index < 0 || index >= (int)r->hdr_->readers) {
       delete r;
       throw std::runtime_error("ShmRing: " + name + " is not a ring or reader index out of range");
     }
@@ -128,6 +136,12 @@ class ShmRing {
   }
 
   void close_ring() { hdr_->closed.store(1, std::memory_order_release); }
+  bool closed() const { return hdr_->closed.load(std::memory_order_acquire) != 0; }
+  // Is the producing process still there?  (EPERM: alive, owned by another user.)
+  bool producer_alive() const {
+    const pid_t pid = (pid_t)hdr_->producer_pid.load(std::memory_order_relaxed);
+    return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM);
+  }
   uint64_t head() const { return hdr_->head.load(std::memory_order_acquire); }
   uint64_t cursor(int i) const { return hdr_->cursor[i].v.load(std::memory_order_acquire); }
   int slots() const { return (int)hdr_->slots; }
@@ -138,8 +152,9 @@ class ShmRing {
     std::atomic<uint64_t> v;
   };
   struct Header {
-    uint64_t magic;
+    std::atomic<uint64_t> magic;
     uint32_t slots, slot_bytes, readers, pad;
+    std::atomic<int64_t> producer_pid;
     alignas(64) std::atomic<uint64_t> head;
     alignas(64) std::atomic<uint64_t> closed;
     Counter cursor[kMaxReaders];

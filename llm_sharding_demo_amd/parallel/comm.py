@@ -583,7 +583,9 @@ class ShmPlanChannel:
         if rt is None or not hasattr(rt, "ShmRing"):
             raise TransportError("native runtime with ShmRing not built")
         self.P, self.R, self.grank = transport.P, transport.R, transport.grank
-        self.timeout_s = timeout_s
+        # round_timeout_s <= 0 means "no watchdog", not "no wait": a publish
+        # into a full ring waits for the slowest follower up to 10 min
+        self.timeout_s = timeout_s if timeout_s and timeout_s > 0 else 600.0
         token = transport.broadcast_object(secrets.token_hex(6) if self.grank == 0 else None, src=0)
         import os
 
@@ -653,10 +655,17 @@ class ShmPlanChannel:
     def recv(self, src: int):
         from ..runtime.plan import PLAN_WORDS
 
-        while True:  # an idle server waits here indefinitely
+        while True:  # an idle server waits here indefinitely ...
             data = self.ring.read(1.0)
             if data is not None:
                 break
+            # ... on a live producer: a rank 0 that died (or closed the ring
+            # without a stop plan) fails the follower instead of leaving it
+            # spinning on a ring nobody will write again
+            if self.ring.closed:
+                raise TransportError("plan ring closed by rank 0")
+            if not self.ring.producer_alive():
+                raise TransportError("rank 0 (the plan ring's producer) is gone")
         import numpy as np
 
         nrec = 4 * PLAN_WORDS
@@ -667,6 +676,11 @@ class ShmPlanChannel:
 
     def flush(self) -> None:
         self.fallback.flush()
+
+    def close(self) -> None:
+        """Rank 0, after the followers' stop plans: end every reader's wait."""
+        for r in self.rings.values():
+            r.close()
 
 
 def make_plan_channel(transport: "_DistTransport", timeout_s: float):
@@ -1233,7 +1247,9 @@ def init_distributed(backend: str, device_type: str, timeout_s: float = 600.0) -
 
 
 def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1,
-                        timeout_s: Optional[float] = None) -> Transport:
+                        timeout_s: Optional[float] = None, loop_ring_bytes: int = 256 << 20) -> Transport:
+    """`loop_ring_bytes`: devloop channel rings, sized by the engine for the
+    largest message an edge carries (LSD_LOOP_RING_MB overrides)."""
     if kind == "rccl":  # native communicator (csrc/comm.cpp), one per (edge, lane)
         import os
 
@@ -1250,7 +1266,7 @@ def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1,
 
         t = IpcLoopTransport(num_stages, replicas, lanes=int(os.environ.get("LSD_LANES", "2")),
                              timeout_s=timeout_s,
-                             ring_bytes=int(os.environ.get("LSD_LOOP_RING_MB", "256")) << 20,
+                             ring_bytes=int(os.environ.get("LSD_LOOP_RING_MB", "0")) << 20 or loop_ring_bytes,
                              spin_limit_s=float(os.environ.get("LSD_LOOP_SPIN_S", "30")))
         t.warmup(device)
         return t

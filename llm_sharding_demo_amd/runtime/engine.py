@@ -167,12 +167,19 @@ class Engine(racecheck.Shared):
             if dev.type == "cuda":
                 dev = torch.device("cuda", torch.cuda.current_device())
             self.devices = [dev]
-            self.transport = make_dist_transport(self.P, kind, dev, self.R, cfg.round_timeout_s)
+            self.transport = make_dist_transport(self.P, kind, dev, self.R, cfg.round_timeout_s,
+                                                 loop_ring_bytes=self._loop_ring_bytes())
             self.replica, self.stage_idx = self.transport.replica, self.transport.rank
             if os.environ.get("LSD_TEST_STALL_RANK") == str(self.rank):
                 self._stall_after = int(os.environ.get("LSD_TEST_STALL_AFTER", "0"))
             self.kv_slots = self._kv_slots([dev], collective=True)
             stage = self._build_stage(self.stage_idx, dev)
+            if os.environ.get("LSD_TEST_CORRUPT_RANK") == str(self.rank):
+                # test hook: a faulty stage (doubled norm gains) whose output
+                # must fail bench.py's token check against one GPU
+                for k, t in stage.w.items():
+                    if k.endswith(("ln_1.weight", "ln_2.weight", "layernorm.weight")):
+                        t.mul_(2.0)
             self.stages = [stage]
             self.workers = [self._worker(stage, self.transport, self.stage_idx)]
             self.fabric = None
@@ -247,10 +254,8 @@ class Engine(racecheck.Shared):
         # run): each takes an equal share of the device's memory instead of a
         # fraction of whatever the ranks initialised before it left free
         share = None
-        if collective and torch.cuda.is_available():
-            import torch.distributed as dist
-
-            per_gpu = -(-dist.get_world_size() // max(1, torch.cuda.device_count()))
+        if collective and torch.cuda.is_available() and any(d.type == "cuda" for d in devices):
+            per_gpu = self._ranks_sharing_device(devices[0])
             if per_gpu > 1:
                 def share(d, n=per_gpu):
                     free, total = torch.cuda.mem_get_info(d)
@@ -271,6 +276,23 @@ class Engine(racecheck.Shared):
             log.warning("KV budget: %d of %d requested slots fit", fits, want)
         return fits
 
+    def _ranks_sharing_device(self, dev: torch.device) -> int:
+        """Dist ranks bound to this very GPU (the single-GPU rehearsal puts
+        several on one): every rank publishes (host, device identity) on the
+        control group and counts its own key.  Independent of how many GPUs
+        each process sees (HIP_VISIBLE_DEVICES) and of the node count."""
+        import socket
+
+        import torch.distributed as dist
+
+        props = torch.cuda.get_device_properties(dev)
+        ident = str(getattr(props, "uuid", "") or "") or ":".join(
+            str(getattr(props, f, "")) for f in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+        key = (socket.gethostname(), ident if ident.strip(":") else str(dev))
+        keys = [None] * dist.get_world_size()
+        dist.all_gather_object(keys, key, group=self.transport.ctrl)
+        return max(1, sum(1 for k in keys if k == key))
+
     def _devloop_fabric(self, dev: torch.device) -> DeviceLoopFabric:
         """Loopback channels sized for the largest message an edge carries:
         one item's prefill rows (a group's chunk tokens, fp32) or decode rows;
@@ -278,14 +300,22 @@ class Engine(racecheck.Shared):
         senders of an 8-stage rehearsal waited for ring space (GPT-2 small P=8:
         287k -> 300k tok/s with 512 MiB rings, profiles/r4_ab_rehearsal.log).
         LSD_LOOP_RING_MB overrides."""
-        cfg, H = self.cfg, self.mcfg.hidden
-        per_seq = cfg.prefill_chunk if cfg.prefill_chunk > 0 else self.max_seq
-        big = self.group_cap * min(per_seq, self.max_seq) * H * 4
-        ring = int(os.environ.get("LSD_LOOP_RING_MB", "0")) << 20 or min(1 << 30, max(64 << 20, 8 * big))
-        ring = max(ring, big + (1 << 20))
-        return DeviceLoopFabric(self.P, dev, lanes=int(os.environ.get("LSD_LANES", "2")), ring_bytes=ring,
-                                timeout=cfg.round_timeout_s,
+        cfg = self.cfg
+        return DeviceLoopFabric(self.P, dev, lanes=int(os.environ.get("LSD_LANES", "2")),
+                                ring_bytes=self._loop_ring_bytes(),
+                                # round_timeout_s <= 0 = no watchdog, not zero-length waits
+                                timeout=cfg.round_timeout_s if cfg.round_timeout_s > 0 else 600.0,
                                 spin_limit_s=float(os.environ.get("LSD_LOOP_SPIN_S", "30")))
+
+    def _loop_ring_bytes(self) -> int:
+        """Device-loopback ring per channel (in-process fabric and the dist-mode
+        rehearsal alike): eight of the largest messages an edge carries -- one
+        item's prefill rows (a group's chunk tokens, fp32) -- within 64 MiB to
+        1 GiB, and never less than one such message plus 1 MiB."""
+        per_seq = self.cfg.prefill_chunk if self.cfg.prefill_chunk > 0 else self.max_seq
+        big = self.group_cap * min(per_seq, self.max_seq) * self.mcfg.hidden * 4
+        ring = int(os.environ.get("LSD_LOOP_RING_MB", "0")) << 20 or min(1 << 30, max(64 << 20, 8 * big))
+        return max(ring, big + (1 << 20))
 
     def _weight_bytes(self, i: int) -> int:
         mc = self.mcfg
@@ -675,6 +705,8 @@ class Engine(racecheck.Shared):
                 self.plan_ch.send_many([g for g in range(rep * self.P, (rep + 1) * self.P) if g],
                                        StepPlan(step=-1, stop=True))
             self.plan_ch.flush()
+            if hasattr(self.plan_ch, "close"):
+                self.plan_ch.close()  # the stop plans stay readable: readers drain first
             self._close_dist()
 
     def _close_dist(self) -> None:

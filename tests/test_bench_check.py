@@ -1,0 +1,66 @@
+"""bench.py at N > 1 checks its own tokens: after the timed region rank 0
+re-generates the first groups of the last session on a 1-stage engine on its
+own device and reports `pipeline_matches_1gpu`; a mismatch exits non-zero.
+The driver's multi-GPU scaling run is the only hardware execution the RCCL
+path gets, so a pipeline producing wrong tokens must not print a number and
+pass (the hop it replaces, `/root/reference/server.py:171-181`, checks
+nothing).  CPU: gloo ranks; GPU: rank processes on one MI355X (devloop)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(world, extra, env_extra=None, timeout=400):
+    port = _port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+    env.update(env_extra or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "1", "--warmup", "0"] + extra
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+CPU = ["--model", "gpt2-test", "--batch", "8", "--prompt", "6", "--gen", "5", "--device", "cpu",
+       "--transport", "gloo"]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_bench_reports_token_check(world):
+    r, out = _bench(world, CPU)
+    assert r.returncode == 0 and out is not None, r.stderr[-3000:]
+    assert out["pipeline_matches_1gpu"] is True, out
+    assert out["check_seqs"] > 0 and out["pg_world_size"] == world, out
+
+
+def test_gloo_bench_corrupted_stage_fails():
+    r, out = _bench(2, CPU, env_extra={"LSD_TEST_CORRUPT_RANK": "1"})
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert out is not None and out["pipeline_matches_1gpu"] is False, out
+    assert out["check_mismatched_seqs"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_devloop_bench_reports_token_check(world):
+    """Rank processes sharing one MI355X over the device-loopback data plane
+    (the rccl code path's rehearsal), GPT-2 small, 2 groups per stage."""
+    r, out = _bench(world, ["--model", "gpt2", "--batch", "16", "--prompt", "16", "--gen", "8",
+                            "--transport", "devloop"], env_extra={"LSD_LOOP_RING_MB": "16"})
+    assert r.returncode == 0 and out is not None, (r.stdout[-2000:], r.stderr[-3000:])
+    assert out["pipeline_matches_1gpu"] is True and out["transport"] == "devloop", out

@@ -86,10 +86,12 @@ def _run(tmp_path, world, device, transport, dp=1, greedy=True, env_extra=None, 
                     eng.shutdown()
         except Exception as e:
             print("FAIL", type(e).__name__, e, flush=True)
-            # a follower whose data plane failed (the stall tests) exits 0: a
+            # a follower whose data plane failed in a stall test exits 0: a
             # non-zero exit makes torchrun kill rank 0 before it prints RESULT;
-            # a rank that could not even build its engine still fails the job
-            code = 3 if "eng" not in dir() else 0
+            # in a healthy run any follower failure (or an engine that could
+            # not even be built) fails the job
+            stall = bool(os.environ.get("LSD_TEST_STALL_RANK"))
+            code = 0 if ("eng" in dir() and stall) else 3
         sys.stdout.flush()
         os._exit(code)  # a stalled peer must not hold the teardown
     """))

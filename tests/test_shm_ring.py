@@ -89,3 +89,38 @@ def test_readers_in_other_processes():
         assert outs == [want, want]
     finally:
         w.unlink()
+
+
+def _create_and_die(name, q):
+    w = rt.ShmRing.create(name, 4, 128, 1)
+    w.publish(b"last words", 1.0)
+    q.put("ok")
+    os._exit(0)  # no close, no unlink: a crashed rank 0
+
+
+def test_reader_detects_dead_producer_and_close():
+    name = _name()
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_create_and_die, args=(name, q))
+    p.start()
+    assert q.get(timeout=30) == "ok"
+    p.join(30)
+    r = rt.ShmRing.attach(name, 0)
+    try:
+        assert r.read(1.0) == b"last words"  # what was published stays readable
+        assert r.read(0.01) is None and not r.closed
+        assert not r.producer_alive()
+    finally:
+        os.unlink("/dev/shm" + name)  # a dead producer leaves its segment behind
+    # a live producer that closes: readers drain, then see the ring closed
+    name2 = _name()
+    w = rt.ShmRing.create(name2, 4, 128, 1)
+    try:
+        r2 = rt.ShmRing.attach(name2, 0)
+        assert r2.producer_alive()
+        w.publish(b"stop", 1.0)
+        w.close()
+        assert r2.read(1.0) == b"stop" and r2.read(1.0) is None and r2.closed
+    finally:
+        w.unlink()

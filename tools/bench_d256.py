@@ -77,6 +77,8 @@ def main():
             N, K, kind = SHAPES[name]
             nbytes = N * K * 2
             nw = max(2, math.ceil((640 << 20) / nbytes))
+            if os.environ.get("D256_WARM"):  # one weight re-used: L2 / MALL-warm W (diagnostic)
+                nw = 1
             ws = [torch.randn(N, K, device=DEV).mul_(0.02).bfloat16() for _ in range(nw)]
             a = torch.randn(M, K, device=DEV).bfloat16()
             x0 = torch.randn(M, N, device=DEV)
@@ -89,10 +91,14 @@ def main():
                 x = x0.clone()
 
                 kind = 3 if bn == 128 else 2
+                if bn >= 1000:  # W-to-VGPR kernel (kind 4), bn = 1000 + variant code
+                    kind, vw = 4, bn - 1000
 
                 def run():
                     C.gemm_set_ring8(r8 & 15)  # read at launch (capture) time
                     C.gemm_set_ring8_flags(r8 >> 4)
+                    if kind == 4:
+                        C.gemm_set_vw(vw)
                     w = ws[it[0] % nw]
                     it[0] += 1
                     if resid:
@@ -115,6 +121,12 @@ def main():
 
             cases = [("ring", 0, 1, int(os.environ.get("D256_BASE_R8", "0")))]
             for v in variants:
+                if v.startswith("vw:"):  # vw:CODE[:S] -- S K splits for the residual shapes
+                    f = [int(x) for x in v[3:].split(":")]
+                    S = f[1] if len(f) > 1 else 1
+                    if S == 1 or resid:
+                        cases.append((f"vw{f[0]}s{S}", 1000 + f[0], S, 0))
+                    continue
                 if v.startswith("r8s:"):  # 8-wave ring, S K splits + in-kernel combine
                     C.gemm_set_ring8(2)
                     if not resid and C.gemm_ring8_tiles(M, N, K, int(v[4:])):
