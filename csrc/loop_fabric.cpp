@@ -43,6 +43,7 @@
 #include <vector>
 
 #include "kernels/loopback.h"
+#include "runtime/loop_handshake.h"
 
 namespace py = pybind11;
 
@@ -59,21 +60,9 @@ struct Fabric;
 // Enqueue mirrors of one channel (each side written by its one owning stage
 // thread / process): in process memory, or in a POSIX shared-memory block
 // when the two ends are different processes on one GPU (loop_chan_attach).
-struct alignas(64) Mirror {
-  std::atomic<uint64_t> send_n, send_end;
-  std::atomic<uint64_t> recv_n, recv_end;
-  // fault injection (tests): sends with index >= stall_from publish nothing
-  std::atomic<uint64_t> stall_from;
-};
-static_assert(sizeof(Mirror) == 64, "one cache line per channel mirror");
-
-void mirror_init(Mirror* m) {
-  m->send_n.store(0);
-  m->send_end.store(0);
-  m->recv_n.store(0);
-  m->recv_end.store(0);
-  m->stall_from.store(~0ull);
-}
+// The handshake itself lives in runtime/loop_handshake.h (HIP-free, TSan-tested).
+using Mirror = lsd_rt::LoopMirror;
+static_assert(LOOP_HEADERS == lsd_rt::kLoopHeaders, "handshake header count");
 
 struct Chan {
   Fabric* fab = nullptr;
@@ -123,8 +112,6 @@ std::string chan_name(const Chan* c) { return "loopback channel " + std::to_stri
 // handshake (module comment).  Several ops on one channel are accounted
 // cumulatively.  Throws on abort or after the fabric timeout.
 void wait_ops(Fabric* f, const Ops& ops) {
-  using clk = std::chrono::steady_clock;
-  const auto t0 = clk::now();
   for (size_t i = 0; i < ops.size(); ++i) {
     const Op& op = ops[i];
     Chan* c = op.ch;
@@ -138,57 +125,25 @@ void wait_ops(Fabric* f, const Ops& ops) {
     for (size_t j = 0; j < i; ++j)
       if (ops[j].ch == c && ops[j].dir == op.dir) {
         ++k;
-        head = lsd_loop_place(head, ops[j].bytes, c->cap) + ops[j].bytes;
+        head = lsd_rt::loop_place(head, ops[j].bytes, c->cap) + ops[j].bytes;
       }
-    for (uint64_t spins = 0;; ++spins) {
-      bool ok;
-      if (op.dir) {  // receive #(recv_n + k) needs send #(recv_n + k) enqueued
-        ok = c->m->send_n.load(std::memory_order_acquire) > c->m->recv_n.load(std::memory_order_relaxed) + k;
-      } else {  // send: header slot + ring bytes freed by already-enqueued receives
-        const uint64_t rn = c->m->recv_n.load(std::memory_order_acquire);
-        const uint64_t rend = c->m->recv_end.load(std::memory_order_acquire);
-        const uint64_t n = c->m->send_n.load(std::memory_order_relaxed) + k;
-        const uint64_t off = lsd_loop_place(head, op.bytes, c->cap);
-        ok = n - rn < LOOP_HEADERS && off + op.bytes - rend <= c->cap;
-      }
-      if (ok) break;
-      if (f->aborted.load(std::memory_order_relaxed))
-        throw std::runtime_error(chan_name(c) + ": data plane aborted");
-      // a short yield spin (the peer is usually microseconds away), then
-      // sleeps: up to 8 stage threads wait at once, and yield-spinning ones
-      // take the host CPUs that the threads they wait for need
-      if (spins < 64) {
-        std::this_thread::yield();
-        continue;
-      }
-      if (std::chrono::duration<double>(clk::now() - t0).count() > f->timeout_s)
-        throw std::runtime_error(chan_name(c) + ": timed out waiting for the peer stage (" +
-                                 std::string(op.dir ? "receive: no matching send" : "send: ring full") +
-                                 ")");
-      std::this_thread::sleep_for(std::chrono::microseconds(spins < 256 ? 5 : 25));
-    }
+    lsd_rt::loop_wait_until(
+        [&] { return op.dir ? lsd_rt::loop_can_recv(c->m, k) : lsd_rt::loop_can_send(c->m, k, head, op.bytes, c->cap); },
+        [&] { return f->aborted.load(std::memory_order_relaxed); }, f->timeout_s,
+        chan_name(c) + ": data plane aborted",
+        chan_name(c) + ": timed out waiting for the peer stage (" +
+            std::string(op.dir ? "receive: no matching send" : "send: ring full") + ")");
   }
 }
 
 // Enqueue one op on `st` (no wait) and advance its side's mirror.
 void launch_op(Fabric* f, const Op& op, void* ptr, hipStream_t st, bool mirror) {
   Chan* c = op.ch;
-  if (op.dir == 0) {
-    const uint64_t n = c->m->send_n.load(std::memory_order_relaxed);
+  if (op.dir == 0)
     hip_check(lsd_loop_send(c->dev, c->ring, ptr, op.bytes, f->dev, st), "loopback send");
-    if (mirror) {
-      const uint64_t end = lsd_loop_place(c->m->send_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
-      c->m->send_end.store(end, std::memory_order_relaxed);
-      c->m->send_n.store(n + 1, std::memory_order_release);
-    }
-  } else {
+  else
     hip_check(lsd_loop_recv(c->dev, c->ring, ptr, op.bytes, f->dev, st), "loopback recv");
-    if (mirror) {
-      const uint64_t end = lsd_loop_place(c->m->recv_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
-      c->m->recv_end.store(end, std::memory_order_release);
-      c->m->recv_n.store(c->m->recv_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
-    }
-  }
+  if (mirror) lsd_rt::loop_advance(c->m, op.dir, op.bytes, c->cap);
 }
 
 // Ops captured inside a hipGraph: replayed with the graph, mirrored here.
@@ -217,24 +172,18 @@ void lsd_loop_io_wait(int64_t io) {
 void lsd_loop_io_done(int64_t io) {
   // advance the mirrors of a launched graph's captured ops (in op order)
   auto* l = reinterpret_cast<IoList*>(io);
-  for (const Op& op : l->ops) {
-    Chan* c = op.ch;
-    if (op.dir == 0) {
-      const uint64_t end = lsd_loop_place(c->m->send_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
-      c->m->send_end.store(end, std::memory_order_relaxed);
-      c->m->send_n.store(c->m->send_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
-    } else {
-      const uint64_t end = lsd_loop_place(c->m->recv_end.load(std::memory_order_relaxed), op.bytes, c->cap) + op.bytes;
-      c->m->recv_end.store(end, std::memory_order_release);
-      c->m->recv_n.store(c->m->recv_n.load(std::memory_order_relaxed) + 1, std::memory_order_release);
-    }
-  }
+  for (const Op& op : l->ops) lsd_rt::loop_advance(op.ch->m, op.dir, op.bytes, op.ch->cap);
 }
 
 void lsd_register_loopback(py::module& m) {
   m.def("loop_state_bytes", [] { return (int64_t)sizeof(LoopChan); });
   m.def("loop_headers", [] { return (int)LOOP_HEADERS; });
   m.def("loop_fabric_create", [](double timeout_s) {
+    // the host mirror of the ring placement must be the device kernels' rule
+    for (uint64_t h : {0ull, 1ull, 255ull, 256ull, 4000ull, 65280ull})
+      for (uint64_t b : {1ull, 256ull, 3000ull})
+        if (lsd_rt::loop_place(h, b, 65536) != lsd_loop_place(h, b, 65536))
+          throw std::logic_error("loop_place differs from the device placement");
     auto* f = new Fabric();
     f->timeout_s = timeout_s;
     void* p = nullptr;
@@ -260,7 +209,7 @@ void lsd_register_loopback(py::module& m) {
     c->fab = f;
     c->own_m = std::make_unique<Mirror>();
     c->m = c->own_m.get();
-    mirror_init(c->m);
+    lsd_rt::loop_mirror_init(c->m);
     c->dev = reinterpret_cast<LoopChan*>(state.data_ptr());
     c->ring = static_cast<uint8_t*>(ring.data_ptr());
     c->cap = (uint64_t)ring.numel();
@@ -426,7 +375,7 @@ void lsd_register_loopback(py::module& m) {
       st.id = c->id;
       st.stall_from = ~0ull;
       hip_check(hipMemcpy(c->dev, &st, sizeof(st), hipMemcpyHostToDevice), "hipMemcpy(chan init)");
-      mirror_init(c->m);
+      lsd_rt::loop_mirror_init(c->m);
     }
     Chan* raw = c.get();
     f->chans.push_back(std::move(c));

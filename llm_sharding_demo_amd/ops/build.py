@@ -63,7 +63,7 @@ def _run(cmd: List[str], verbose: bool) -> None:
 
 def headers() -> List[str]:
     out = []
-    for d in (os.path.join(CSRC, "kernels"), CSRC):
+    for d in (os.path.join(CSRC, "kernels"), CSRC, os.path.join(CSRC, "runtime")):
         for fn in sorted(os.listdir(d)):
             if fn.endswith(".h"):
                 out.append(os.path.join(d, fn))
