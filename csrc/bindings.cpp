@@ -65,7 +65,8 @@ void lsd_gemv_set_nt(int v);
 hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st);
 hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                       const int* topk, const int* greedy, const long long* seeds,
-                      long long* step, int* out, int advance, const int* active, hipStream_t st);
+                      long long* step, int* out, int advance, const int* active, int* pos,
+                      hipStream_t st);
 }
 
 namespace {
@@ -581,7 +582,8 @@ torch::Tensor attn_prefill(torch::Tensor q, torch::Tensor kc, torch::Tensor vc,
 void sample_launch(const torch::Tensor& logits, int64_t V, const torch::Tensor& temp,
                    const torch::Tensor& topk, const torch::Tensor& greedy, const torch::Tensor& seeds,
                    torch::Tensor& step, torch::Tensor& out, bool advance,
-                   const c10::optional<torch::Tensor>& active = c10::nullopt) {
+                   const c10::optional<torch::Tensor>& active = c10::nullopt,
+                   const c10::optional<torch::Tensor>& pos = c10::nullopt) {
   need(logits, torch::kFloat32, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && V <= logits.size(1) && V >= 1, "logits [B, >=V]");
   TORCH_CHECK(logits.stride(0) % 4 == 0 && logits.size(1) % 4 == 0, "logits row length must be a multiple of 4");
@@ -603,11 +605,17 @@ void sample_launch(const torch::Tensor& logits, int64_t V, const torch::Tensor& 
     TORCH_CHECK(active->numel() == B && active->is_contiguous(), "active must be contiguous int32 [B]");
     act = active->data_ptr<int>();
   }
+  int* pp = nullptr;
+  if (pos.has_value()) {
+    need(*pos, torch::kInt32, "pos");
+    TORCH_CHECK(pos->numel() == B && pos->is_contiguous(), "pos must be contiguous int32 [B]");
+    pp = pos->data_ptr<int>();
+  }
   check_hip(lsd_sample(logits.data_ptr<float>(), logits.stride(0), B, V, temp.data_ptr<float>(),
                        topk.data_ptr<int>(), greedy.data_ptr<int>(),
                        reinterpret_cast<const long long*>(seeds.data_ptr<int64_t>()),
                        reinterpret_cast<long long*>(step.data_ptr<int64_t>()),
-                       out.data_ptr<int>(), advance ? 1 : 0, act, cur_stream()), "sample");
+                       out.data_ptr<int>(), advance ? 1 : 0, act, pp, cur_stream()), "sample");
 }
 
 torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
@@ -618,12 +626,13 @@ torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch:
 }
 
 // Decode-step form: the sampled ids go straight into `out` (the token-return
-// vector) and each row's sampler counter advances by active[row] (1 without
-// `active`) in the same kernel.
+// vector) and each row's sampler counter -- and, given `pos`, the row's KV
+// position of the last stage -- advances by active[row] (1 without `active`)
+// in the same kernel.
 void sample_into(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
                  torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step, torch::Tensor out,
-                 c10::optional<torch::Tensor> active) {
-  sample_launch(logits, V, temp, topk, greedy, seeds, step, out, true, active);
+                 c10::optional<torch::Tensor> active, c10::optional<torch::Tensor> pos) {
+  sample_launch(logits, V, temp, topk, greedy, seeds, step, out, true, active, pos);
 }
 
 }  // namespace
@@ -647,7 +656,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_oproj", &attn_oproj);
   m.def("sample", &sample);
-  m.def("sample_into", &sample_into);
+  m.def("sample_into", &sample_into, py::arg("logits"), py::arg("V"), py::arg("temp"), py::arg("topk"),
+        py::arg("greedy"), py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("active"),
+        py::arg("pos") = py::none());
   m.def("gemv", &gemv);
   // GEMV weight stream with non-temporal loads (A/B knob, LSD_GEMV_NT)
   m.def("gemv_set_nt", [](int64_t v) { lsd_gemv_set_nt((int)v); });

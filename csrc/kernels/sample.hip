@@ -91,6 +91,17 @@ __device__ __forceinline__ void for_row(const float* x, int V, F&& f) {
   }
 }
 
+// The decode step's per-row counter advance, after the draw: the sampler
+// counter and (pos != null) the row's KV position both move by active[row]
+// (1 when active is null; pad rows stay put) -- one kernel instead of two
+// extra add kernels per group-step.
+__device__ __forceinline__ void advance_row(long long* step, int* pos, const int* active, int row,
+                                            long long step_r) {
+  const int a = active ? active[row] : 1;
+  step[row] = step_r + a;
+  if (pos) pos[row] += a;
+}
+
 __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ logits, long ld,
                                                     int V, const float* __restrict__ temp,
                                                     const int* __restrict__ topk,
@@ -98,7 +109,8 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
                                                     const long long* __restrict__ seeds,
                                                     long long* __restrict__ step,
                                                     int* __restrict__ out, int advance,
-                                                    const int* __restrict__ active) {
+                                                    const int* __restrict__ active,
+                                                    int* __restrict__ pos) {
   __shared__ unsigned hist[4096];
   __shared__ float cval[SMAX];
   __shared__ int cidx[SMAX];
@@ -133,7 +145,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
       for (int w = 1; w < NT / 64; ++w)
         if (redv[w] > best || (redv[w] == best && redi[w] < bi)) { best = redv[w]; bi = redi[w]; }
       out[row] = bi;
-      if (advance) step[row] = step_r + (active ? active[row] : 1);  // all threads read step[row] before the barrier
+      if (advance) advance_row(step, pos, active, row, step_r);  // all threads read step[row] before the barrier
     }
     return;
   }
@@ -381,7 +393,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     const int win = __shfl(pick & 1 ? ix[1] : ix[0], pick >> 1, 64);
     if (tid == 0) {
       out[row] = win;
-      if (advance) step[row] = step_r + (active ? active[row] : 1);
+      if (advance) advance_row(step, pos, active, row, step_r);
     }
     return;
   }
@@ -436,7 +448,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     }
     if (tid == 0) {
       out[row] = cidx[pick];
-      if (advance) step[row] = step_r + (active ? active[row] : 1);
+      if (advance) advance_row(step, pos, active, row, step_r);
     }
   }
 }
@@ -451,10 +463,10 @@ using namespace lsd;
 extern "C" hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                                  const int* topk, const int* greedy, const long long* seeds,
                                  long long* step, int* out, int advance, const int* active,
-                                 hipStream_t st) {
+                                 int* pos, hipStream_t st) {
   if (B == 0) return hipSuccess;
   if (ld % 4 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(NT), 0, st, logits, ld, V, temp, topk, greedy,
-                     seeds, step, out, advance, active);
+                     seeds, step, out, advance, active, pos);
   return hipGetLastError();
 }

@@ -108,10 +108,13 @@ class ReferenceBackend(Backend):
         return ref.sample(logits, samp.temperature, samp.top_k, samp.greedy,
                           samp.uniforms(), vocab)
 
-    def sample_into(self, logits, samp, vocab: int, out) -> None:
-        """Decode step: sampled ids into `out`, then the sampler counters advance."""
+    def sample_into(self, logits, samp, vocab: int, out, meta=None) -> None:
+        """Decode step: sampled ids into `out`, then the sampler counters (and,
+        given the decode `meta`, its positions) advance."""
         out.copy_(self.sample(logits, samp, vocab))
         samp.advance()
+        if meta is not None:
+            meta.advance()
 
     def gather_rows(self, x, idx):
         return x.index_select(0, idx.long())

@@ -543,10 +543,12 @@ class HipBackend(Backend):
         return self.C.sample(logits, vocab, samp.temperature, samp.top_k, samp.greedy,
                              samp.seeds, samp.step)
 
-    def sample_into(self, logits, samp, vocab: int, out) -> None:
+    def sample_into(self, logits, samp, vocab: int, out, meta=None) -> None:
         # one kernel: draw into `out`, advance the per-row sampler counters
+        # and (meta given) the decode batch's positions
         self.C.sample_into(logits, vocab, samp.temperature, samp.top_k, samp.greedy,
-                           samp.seeds, samp.step, out, getattr(samp, "active", None))
+                           samp.seeds, samp.step, out, getattr(samp, "active", None),
+                           meta.token_pos if meta is not None else None)
 
     def gather_rows(self, x, idx):
         return x.index_select(0, idx.long())

@@ -812,13 +812,14 @@ class StageWorker(racecheck.Shared):
                 self._recv(inp, self.r - 1, "fwd", lane, stage=gs.wire_buf(self, gp.b), capture=True)
             meta = gs.meta(gp.b, gp.ctxb)
             out = self.stage.forward(meta, inp, head=True, variant=gp.g & 1)
-            meta.advance()
             if not self.last:
+                meta.advance()
                 if io:
                     self._send(out, self.r + 1, "fwd", lane, capture=True)
                 return out
             samp = gs.samp(gp.b)
-            self.stage.backend.sample_into(out, samp, self.stage.cfg.vocab_size, gs.tokret[: gp.b])
+            # the sampler kernel also advances this stage's positions (no add kernel)
+            self.stage.backend.sample_into(out, samp, self.stage.cfg.vocab_size, gs.tokret[: gp.b], meta)
             if io:
                 self._send(gs.tokret[: gp.b], 0, "ret", lane, capture=True)
             return gs.tokret[: gp.b]

@@ -686,6 +686,11 @@ def test_sampler(C):
     st3 = step.clone()
     C.sample_into(logits, V, temp, topk, greedy, seeds, st3, buf[:B], act)
     assert buf[:B].cpu().tolist() == exp.tolist() and torch.equal(st3, step + act)
+    # the last stage's decode positions advance in the same kernel
+    pos = torch.arange(B, dtype=torch.int32, device=DEV) + 100
+    st4 = step.clone()
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st4, buf[:B], act, pos)
+    assert torch.equal(st4, step + act) and torch.equal(pos, torch.arange(B, device=DEV).int() + 100 + act)
     for r in range(B):
         k = 1 if greedy[r] else int(topk[r])
         assert int(out[r]) in set(torch.topk(logits[r, :V], k).indices.tolist())

@@ -95,6 +95,8 @@ def _create_and_die(name, q):
     w = rt.ShmRing.create(name, 4, 128, 1)
     w.publish(b"last words", 1.0)
     q.put("ok")
+    q.close()
+    q.join_thread()  # flush the queue's feeder thread before the hard exit
     os._exit(0)  # no close, no unlink: a crashed rank 0
 
 
