@@ -1872,26 +1872,31 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <int MT, int SA>
+template <int MT, int SA, int BN>
 constexpr int vw_smem() {
-  return SA * MT * 16 * 128 > MT * 16 * 68 * 4 ? SA * MT * 16 * 128 : MT * 16 * 68 * 4;
+  return SA * MT * 16 * 128 > MT * 16 * (BN + 4) * 4 ? SA * MT * 16 * 128 : MT * 16 * (BN + 4) * 4;
 }
 
-template <int EPI, int MT, int DW, int SA>
-__global__ __launch_bounds__(256) void gemm_vw_kernel(GemmParams p, int tiles_m, int tiles_n) {
-  constexpr int BM = 16 * MT;
-  constexpr int A_STEP = BM * 128;  // bytes of one [BM][64 k] A image
-  constexpr int AG = BM / 32;       // LDS-DMA (1 KiB) per wave per step
-  static_assert(MT % 2 == 0 && MT >= 2 && MT <= 8, "BM in {32, 64, 96, 128}");
+// NWV waves (4 or 8): the tile is BM x (16 NWV) columns, wave w owns columns
+// [16 w, 16 w + 16) and all BM rows; with 8 waves two share each SIMD (one
+// wave's MFMAs cover the other's issue and LDS latency).
+template <int EPI, int MT, int DW, int SA, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) void gemm_vw_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int BM = 16 * MT, BN = 16 * NWV;
+  constexpr int A_STEP = BM * 128;     // bytes of one [BM][64 k] A image
+  constexpr int AG = BM * 128 / 1024 / NWV;  // LDS-DMA (1 KiB) per wave per step
+  static_assert(NWV == 4 || NWV == 8, "4 or 8 waves");
+  static_assert(AG * 1024 * NWV == A_STEP && AG >= 1, "A image split evenly over the waves");
+  static_assert(MT >= 2 && MT <= 8, "BM in 32..128");
   static_assert(SA >= 2 && SA <= 6 && DW >= 1 && DW <= 8, "ring depths");
   static_assert((SA - 2) * AG + 2 * (SA - 1) <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[vw_smem<MT, SA>()];  // A ring; then the C tile
+  __shared__ __attribute__((aligned(16))) char smem[vw_smem<MT, SA, BN>()];  // A ring; then the C tile
 
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int per_split = tiles_m * tiles_n;
   const int split = bid / per_split, t = bid % per_split;
   const int tm = t % tiles_m, tn = t / tiles_m;  // M-fastest: a W panel's row tiles share an XCD
-  const int m0 = tm * BM, n0 = tn * 64;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int KT = p.K / 64;
   const int kb = (int)((long)KT * split / p.splits), ke = (int)((long)KT * (split + 1) / p.splits);
   const int nk = ke - kb;
@@ -1909,7 +1914,7 @@ __global__ __launch_bounds__(256) void gemm_vw_kernel(GemmParams p, int tiles_m,
 
   auto stage_a = [&](int s) {  // step s (clamped into the split) -> slot s % SA
     const int k = kb + min(s, nk - 1);
-    stage_rows<BM, 4>(smem + (s % SA) * A_STEP, p.A, p.lda, m0, p.M - 1, k * 64, w);
+    stage_rows<BM, NWV>(smem + (s % SA) * A_STEP, p.A, p.lda, m0, p.M - 1, k * 64, w);
   };
   auto load_w = [&](int s, bf16x8 (&wv)[2]) {
     const bf16* src = s < nk ? wrow + (long)s * 64 : wdummy;
@@ -1959,14 +1964,14 @@ __global__ __launch_bounds__(256) void gemm_vw_kernel(GemmParams p, int tiles_m,
   // every wave's fragment reads retired before the C tile overwrites the ring
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
   __syncthreads();
-  constexpr int CLD = 64 + 4;
+  constexpr int CLD = BN + 4;
   float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int q = 0; q < 4; ++q) ct[(i * 16 + 4 * g + q) * CLD + 16 * w + r] = acc[i][q];
   __syncthreads();
-  ct_store<EPI, 64, BM, 256>(p, ct, m0, n0, split);
+  ct_store<EPI, BN, BM, NWV * 64>(p, ct, m0, n0, split);
   LSD_STAMP(2)
 }
 
@@ -2088,19 +2093,19 @@ static hipError_t launch_d256(const GemmParams& p, int kind, int* cnt, float* ws
 }
 
 // gemm_vw variant (lsd_gemm_set_vw): rows per tile (MT = 16-row MFMA tiles), W k-steps in
-// flight (DW), A ring slots (SA)
-static int g_vw_mt = 8, g_vw_dw = 6, g_vw_sa = 4;
+// flight (DW), A ring slots (SA), waves (NWV: 64 or 128-column tiles)
+static int g_vw_mt = 8, g_vw_dw = 6, g_vw_sa = 4, g_vw_nw = 4;
 
 static bool vw_ok(int M, int N, int K) { return M >= 1 && M <= 256 && K % 64 == 0 && N % 64 == 0; }
 static int vw_tiles_m(int M) { return (M + 16 * g_vw_mt - 1) / (16 * g_vw_mt); }
 
-template <int EPI, int MT>
+template <int EPI, int MT, int NWV>
 static hipError_t launch_vw_mt(const GemmParams& p, hipStream_t st) {
-  const int tm = (p.M + 16 * MT - 1) / (16 * MT), tn = p.N / 64;
-  const dim3 grid(tm * tn * p.splits), block(256);
+  const int tm = (p.M + 16 * MT - 1) / (16 * MT), tn = (p.N + 16 * NWV - 1) / (16 * NWV);
+  const dim3 grid(tm * tn * p.splits), block(NWV * 64);
 #define LSD_VW(DW, SA)                                                                               \
   if (g_vw_dw == DW && g_vw_sa == SA) {                                                              \
-    hipLaunchKernelGGL((gemm_vw_kernel<EPI, MT, DW, SA>), grid, block, 0, st, p, tm, tn);            \
+    hipLaunchKernelGGL((gemm_vw_kernel<EPI, MT, DW, SA, NWV>), grid, block, 0, st, p, tm, tn);       \
     return hipGetLastError();                                                                        \
   }
   LSD_VW(4, 3) LSD_VW(6, 4) LSD_VW(8, 4) LSD_VW(8, 6)
@@ -2111,10 +2116,18 @@ static hipError_t launch_vw_mt(const GemmParams& p, hipStream_t st) {
 template <int EPI>
 static hipError_t launch_vw(const GemmParams& p, hipStream_t st) {
   if (!vw_ok(p.M, p.N, p.K) || (p.splits > 1 && EPI != EPI_SLAB)) return hipErrorInvalidValue;
+  if (g_vw_nw == 8) {
+    if (EPI == EPI_SILU_MUL && p.N % 128) return hipErrorInvalidValue;  // gate/up pairs inside a tile
+    switch (g_vw_mt) {
+      case 4: return launch_vw_mt<EPI, 4, 8>(p, st);
+      case 8: return launch_vw_mt<EPI, 8, 8>(p, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (g_vw_mt) {
-    case 4: return launch_vw_mt<EPI, 4>(p, st);
-    case 6: return launch_vw_mt<EPI, 6>(p, st);
-    case 8: return launch_vw_mt<EPI, 8>(p, st);
+    case 4: return launch_vw_mt<EPI, 4, 4>(p, st);
+    case 6: return launch_vw_mt<EPI, 6, 4>(p, st);
+    case 8: return launch_vw_mt<EPI, 8, 4>(p, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2219,12 +2232,14 @@ extern "C" void lsd_gemm_set_ring8(int v) { g_ring8 = (v == 1 || v == 2) ? v : 0
 extern "C" void lsd_gemm_set_ring8_flags(int v) { g_ring8_flags = v & 7; }
 extern "C" void lsd_gemm_set_ring8_pack(int v) { g_ring8_pack = v & 3; }
 extern "C" void lsd_gemm_set_d256_slots(int v) { g_d256_slots = v < 2 ? 2 : (v > 4 ? 4 : v); }
-// gemm_vw variant: code = MT * 100 + DW * 10 + SA (e.g. 864: 128 rows, 6 W steps, 4 A slots)
+// gemm_vw variant: code = NWV * 1000 + MT * 100 + DW * 10 + SA (e.g. 4864: 4 waves, 128 rows,
+// 6 W steps, 4 A slots; 8464: 8 waves x 16 columns, 64 rows); a 3-digit code means 4 waves
 extern "C" int lsd_gemm_set_vw(int code) {
-  const int mt = code / 100, dw = code / 10 % 10, sa = code % 10;
-  const bool ok = (mt == 4 || mt == 6 || mt == 8) &&
+  const int nw = code >= 1000 ? code / 1000 : 4, mt = code / 100 % 10, dw = code / 10 % 10, sa = code % 10;
+  const bool ok = (nw == 4 ? (mt == 4 || mt == 6 || mt == 8) : (nw == 8 && (mt == 4 || mt == 8))) &&
                   ((dw == 4 && sa == 3) || (dw == 6 && sa == 4) || (dw == 8 && sa == 4) || (dw == 8 && sa == 6));
   if (!ok) return -1;
+  g_vw_nw = nw;
   g_vw_mt = mt;
   g_vw_dw = dw;
   g_vw_sa = sa;

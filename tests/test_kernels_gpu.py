@@ -362,10 +362,11 @@ def test_d256_gemm_epilogues(D256, CNT, M, K, splits):
     assert int(CNT.abs().sum()) == 0  # every ticket re-armed
 
 
-@pytest.fixture(params=[864, 884, 843, 886, 664, 684, 464])
+@pytest.fixture(params=[864, 884, 843, 886, 664, 684, 464, 8464, 8864, 8484, 8443])
 def VW(C, request):
-    """gemm_vw_kernel variants (launch kind 4): MT * 100 + DW * 10 + SA =
-    16-row tiles per workgroup, W k-steps in flight in VGPRs, A ring slots."""
+    """gemm_vw_kernel variants (launch kind 4): [NWV *1000 +] MT * 100 + DW * 10 + SA =
+    [8 waves x 16 columns,] 16-row tiles per workgroup, W k-steps in flight in
+    VGPRs, A ring slots."""
     C.gemm_set_vw(request.param)
     yield C
     C.gemm_set_vw(864)
