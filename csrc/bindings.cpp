@@ -233,8 +233,10 @@ torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, int64_t tiled, int64_
 }
 
 // x += a @ w^T + bias.  Decode path: any split, combined in-kernel -- or,
-// with defer, like the tiled path with splits > 1: returns the fp32 partial
-// slabs [splits, M, N] (bias not applied) that the next norm folds in.
+// with defer, like the tiled path with splits > 1: returns the partial slabs
+// [splits, M, N] (bias not applied) that the next norm folds in.  defer with
+// one split (prefill): the GEMM writes its output as one bf16 slab instead of
+// a read-modify-write of the fp32 residual stream.
 c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
                                               c10::optional<torch::Tensor> bias, torch::Tensor x,
                                               int64_t splits, int64_t tiled,
@@ -245,7 +247,7 @@ c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
               "residual x must be contiguous [M, N]");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "residual x must be 16-byte aligned");
   if (p.M == 0) return c10::nullopt;
-  if ((tiled || defer) && splits > 1) {
+  if ((tiled || defer) && (splits > 1 || defer)) {
     // bf16 partial slabs (LSD_SLAB_BF16=0: fp32): half the bytes the GEMM
     // writes and the next norm reads, each partial rounded once to bf16 --
     // the precision of a bf16 GEMM output, folded into the fp32 residual.

@@ -127,6 +127,9 @@ class HipBackend(Backend):
     # microbatches: 41.2k vs 39.7k tok/s on the tiled kernel (GPT-2 XL, 2 x 256)
     SK_MAX_M = int(os.environ.get("LSD_SK_MAX_M", "256"))
     DEFER_RESID = os.environ.get("LSD_DEFER_RESID", "1") == "1"
+    # prefill residual projections: bf16 slab + fold in the next norm
+    # (LSD_PREFILL_SLAB=0: fp32 read-modify-write in the GEMM epilogue)
+    PREFILL_SLAB = os.environ.get("LSD_PREFILL_SLAB", "1") == "1"
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
     # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:
@@ -519,6 +522,11 @@ class HipBackend(Backend):
         # decode split-K: hand the S partial slabs to the next norm (which
         # reads the rows anyway) instead of a last-arriver reduce in the GEMM
         defer = self.DEFER_RESID and not tiled and splits > 1
+        if self.PREFILL_SLAB and tiled and splits == 1 and not getattr(self, "decode", True) and M > 256:
+            # prefill: the GEMM writes one bf16 slab (the norm that follows folds
+            # it into the fp32 stream) instead of an fp32 read-modify-write of
+            # the residual in its epilogue
+            defer = True
         slab = self.C.linear_residual(a, w, b, r.x, splits, tiled, self.counters, defer)
         if slab is not None:
             r.pending.append((slab, b))

@@ -76,17 +76,19 @@ def _fp32_slabs(C):
 # 8-wave decode ring (256 / 130 rows), split-K decode kernel (64 rows, deferred) and the
 # 256x256 prefill-class kernel (1024 rows x 6 splits = 168 tiles)
 @pytest.mark.parametrize("tiled,M,splits", [(True, 256, 3), (True, 256, 5), (True, 130, 3), (False, 64, 5),
-                                            (True, 1024, 6)])
+                                            (True, 1024, 6), (True, 1024, 1), (True, 3000, 1)])
 def test_linear_residual_bf16_slabs(C, CNT, tiled, M, splits):
     """bf16 partial slabs: each split's partial rounded once to bf16 (a bf16
-    GEMM output's precision), folded into the fp32 residual by the norm."""
+    GEMM output's precision), folded into the fp32 residual by the norm.  One
+    split with defer: the prefill form (the GEMM writes one bf16 slab instead
+    of a read-modify-write of the fp32 residual)."""
     C.gemm_set_slab_bf16(1)
     N, K = 1600, 1600
     a, w, bias = bf(M, K, seed=8), bf(N, K, scale=0.05, seed=9), bf(N, scale=0.1, seed=10)
     x = torch.randn(M, N, device=DEV)
     y = ref.linear(a, w, bias)
     x_ref = x + y
-    slab = C.linear_residual(a, w, bias, x, splits, tiled, CNT, not tiled)
+    slab = C.linear_residual(a, w, bias, x, splits, tiled, CNT, not tiled or splits == 1)
     assert slab is not None and slab.dtype == torch.bfloat16 and slab.shape == (splits, M, N)
     C.norm(x, slab, bias, None, None, 0.0, True, None, False)
     # error of S bf16 roundings of partials of |y| / sqrt(S)-ish size
