@@ -31,8 +31,6 @@ void lsd_gemm_set_ring8(int v);
 void lsd_gemm_set_ring8_flags(int v);
 void lsd_gemm_set_ring8_pack(int v);
 int lsd_gemm_d256_bn(int kind, int M, int N, int K);
-int lsd_gemm_set_vw(int code);
-int lsd_gemm_vw_tiles_m(int M);
 int lsd_gemm_ring8_tiles(int M, int N, int K, int S);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
@@ -133,12 +131,8 @@ GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, int64_t t
   p.M = a.size(0); p.N = w.size(0); p.K = a.size(1);
   p.splits = 1;
   TORCH_CHECK(p.N % 16 == 0, "N must be a multiple of 16 (pad the weight), got ", p.N);
-  TORCH_CHECK(tiled >= 0 && tiled <= 4,
-              "GEMM kind must be 0 (split-K), 1 (tiled), 2 / 3 (256-row), 4 (W-to-VGPR decode), got ", tiled);
-  if (tiled == 4)
-    TORCH_CHECK(p.M >= 1 && p.M <= 256 && p.N % 64 == 0,
-                "W-to-VGPR decode GEMM needs 1 <= M <= 256 and N % 64 == 0, got M ", p.M, " N ", p.N);
-  if (tiled == 2 || tiled == 3)
+  TORCH_CHECK(tiled >= 0 && tiled <= 3, "GEMM kind must be 0 (split-K), 1 (tiled), 2 / 3 (256-row), got ", tiled);
+  if (tiled >= 2)
     TORCH_CHECK(p.M >= 1 && p.M <= 256, "256-row decode GEMM needs 1 <= M <= 256, got ", p.M);
   if (tiled) {
     TORCH_CHECK(p.K % 64 == 0, "tiled GEMM needs K % 64 == 0, got ", p.K);
@@ -161,9 +155,7 @@ void run_gemm(GemmParams& p, int epi, int64_t tiled, int64_t splits,
   int* cnt = nullptr;
   float* ws = nullptr;
   torch::Tensor wsbuf;
-  TORCH_CHECK(tiled != 4 || splits == 1 || epi == EPI_SLAB, what,
-              ": the W-to-VGPR decode GEMM splits K only into residual slabs");
-  if (tiled && tiled != 4 && splits > 1 && epi != EPI_SLAB) {
+  if (tiled && splits > 1 && epi != EPI_SLAB) {
     // tiled split-K with an in-kernel combine: the 256-row decode kernel
     // (gemm_d256, kind 2 / 3) or the 8-wave 128x64 ring (kind 1) -- ticket
     // counters + fp32 partial tiles per split
@@ -686,11 +678,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("gemm_set_ring8_flags", [](int64_t v) { lsd_gemm_set_ring8_flags((int)v); });
   m.def("gemm_set_ring8_pack", [](int64_t v) { lsd_gemm_set_ring8_pack((int)v); });
-  // W-to-VGPR decode GEMM (launch kind 4) variant: MT * 100 + DW * 10 + SA (gemm.hip gemm_vw_kernel)
-  m.def("gemm_set_vw", [](int64_t code) {
-    TORCH_CHECK(lsd_gemm_set_vw((int)code) == 0, "unsupported gemm_vw variant ", code);
-  });
-  m.def("gemm_vw_tiles_m", [](int64_t M) { return lsd_gemm_vw_tiles_m((int)M); });
   m.def("gemm_d256_bn", [](int64_t kind, int64_t M, int64_t N, int64_t K) {
     return lsd_gemm_d256_bn((int)kind, (int)M, (int)N, (int)K);
   });

@@ -25,8 +25,6 @@
 // store, residual add into the fp32 residual stream, split-K slab, and the
 // QKV epilogue that applies RoPE (Llama) and scatters K/V straight into the
 // shard-local KV cache at (slot, position).
-#include <type_traits>
-
 #include "common.h"
 #include "gemm_params.h"
 
@@ -1837,143 +1835,12 @@ __global__ __launch_bounds__(512) void gemm_d256_kernel(GemmParams p, int* __res
   LSD_STAMP(3)
 }
 
-// ---------------------------------------------------------------------------
-// Decode GEMM at 65-256 rows with the weights streamed straight to VGPRs
-// ---------------------------------------------------------------------------
-// The LDS rings above stage BOTH operands by LDS-DMA and read both back with
-// ds_read: per 64-k step a 128x64 tile issues 24 LDS-DMA instructions and 64
-// fragment reads per CU, and keeps two steps (48 KB) in flight -- at ~1.1 us
-// issue-to-landed under load that caps a CU near 45 GB/s (GPT-2 XL QKV at 256
-// rows: 13.3 us with the weights L2-warm, 15.6 cold; profiles/r5_*).  Here:
-//   * 4 waves, wave w owns columns [16 w, 16 w + 16) of the 64-column tile and
-//     ALL BM = 16 * MT rows, so every W fragment is needed by exactly one wave:
-//     it is loaded HBM -> VGPRs (16 B per lane, fragment-shaped) DW k-steps
-//     ahead, never staged through LDS (gemm_sk's design, guide §5 'GEMV /
-//     decode weights', extended past 128 rows);
-//   * the A operand (shared by the 4 waves) goes through an SA-slot LDS ring
-//     by LDS-DMA in full 128-B lines (the [BM][64 k] lds_frag image), SA - 1
-//     steps in flight;
-//   * in flight per CU: DW x 8 KB of W plus (SA - 1) x BM x 128 B of A (DW 8,
-//     SA 4, BM 128: 112 KB), against 48 KB for the ring.
-// Issue order per step s: A(s + SA - 1) [AG LDS-DMA per wave], then W(s + DW)
-// [2 loads].  Everything is issued every step (past the K range: W re-reads
-// a line of A, which is L2-hot, and A re-stages a valid step), so the
-// counted wait that retires A(s) -- and the older W(s) with it -- is the
-// same at every step: vmcnt((SA - 2) * AG + 2 * min(s, SA - 1)).  One raw
-// s_barrier per step publishes A(s) and proves the slot of step s - 1 free.
-// K splits (p.splits > 1) only for EPI_SLAB (residual projections: the next
-// norm folds the slabs).
-// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
-
-template <int MT, int SA, int BN>
-constexpr int vw_smem() {
-  return SA * MT * 16 * 128 > MT * 16 * (BN + 4) * 4 ? SA * MT * 16 * 128 : MT * 16 * (BN + 4) * 4;
-}
-
-// NWV waves (4 or 8): the tile is BM x (16 NWV) columns, wave w owns columns
-// [16 w, 16 w + 16) and all BM rows; with 8 waves two share each SIMD (one
-// wave's MFMAs cover the other's issue and LDS latency).
-template <int EPI, int MT, int DW, int SA, int NWV = 4>
-__global__ __launch_bounds__(NWV * 64) void gemm_vw_kernel(GemmParams p, int tiles_m, int tiles_n) {
-  constexpr int BM = 16 * MT, BN = 16 * NWV;
-  constexpr int A_STEP = BM * 128;     // bytes of one [BM][64 k] A image
-  constexpr int AG = BM * 128 / 1024 / NWV;  // LDS-DMA (1 KiB) per wave per step
-  static_assert(NWV == 4 || NWV == 8, "4 or 8 waves");
-  static_assert(AG * 1024 * NWV == A_STEP && AG >= 1, "A image split evenly over the waves");
-  static_assert(MT >= 2 && MT <= 8, "BM in 32..128");
-  static_assert(SA >= 2 && SA <= 6 && DW >= 1 && DW <= 8, "ring depths");
-  static_assert((SA - 2) * AG + 2 * (SA - 1) <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[vw_smem<MT, SA, BN>()];  // A ring; then the C tile
-
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_split = tiles_m * tiles_n;
-  const int split = bid / per_split, t = bid % per_split;
-  const int tm = t % tiles_m, tn = t / tiles_m;  // M-fastest: a W panel's row tiles share an XCD
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int KT = p.K / 64;
-  const int kb = (int)((long)KT * split / p.splits), ke = (int)((long)KT * (split + 1) / p.splits);
-  const int nk = ke - kb;
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  LSD_STAMP(0)
-
-  // this lane's W row (clamped: a partial last tile re-reads row N-1, never stored)
-  const bf16* wrow = p.W + (long)min(n0 + 16 * w + r, p.N - 1) * p.ldw + (long)kb * 64 + 8 * g;
-  const bf16* wdummy = p.A + 8 * g + (long)min(r, p.M - 1) * p.lda;  // L2-hot, never consumed
-
-  f32x4 acc[MT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto stage_a = [&](int s) {  // step s (clamped into the split) -> slot s % SA
-    const int k = kb + min(s, nk - 1);
-    stage_rows<BM, NWV>(smem + (s % SA) * A_STEP, p.A, p.lda, m0, p.M - 1, k * 64, w);
-  };
-  auto load_w = [&](int s, bf16x8 (&wv)[2]) {
-    const bf16* src = s < nk ? wrow + (long)s * 64 : wdummy;
-    wv[0] = ld8(src);
-    wv[1] = ld8(src + 32);
-  };
-
-  bf16x8 wv[DW][2];
-  if (nk > 0) {
-#pragma unroll
-    for (int j = 0; j < DW; ++j) load_w(j, wv[j]);
-#pragma unroll
-    for (int j = 0; j < SA - 1; ++j) stage_a(j);
-  }
-  // one k-step: retire A(s) (and the older W(s)) with the counted wait
-  // WAIT, publish, refill the slot of step s - 1, compute, reload the W set
-  auto step = [&](int s, bf16x8 (&w_s)[2], auto wait) {
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(decltype(wait)::value));
-    __builtin_amdgcn_s_barrier();
-    stage_a(s + SA - 1);
-    const char* ta = smem + (s % SA) * A_STEP;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[MT];
-#pragma unroll
-      for (int i = 0; i < MT; ++i) af[i] = lds_frag(ta, i * 16 + r, kk * 4 + g);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) acc[i] = mfma16(af[i], w_s[kk], acc[i]);
-    }
-    load_w(s + DW, w_s);  // the register set just consumed takes step s + DW
-  };
-  // steps 0 .. SA-2 peeled (fewer loads younger than A(s) than in steady state)
-  // so the steady loop's wait is one immediate; W set of step s = wv[s % DW]
-  static_for<0, SA - 1>([&](auto j) {
-    if (j < nk) step(j, wv[j % DW], std::integral_constant<int, (SA - 2) * AG + 2 * decltype(j)::value>{});
-  });
-  constexpr int WAIT = (SA - 2) * AG + 2 * (SA - 1);
-  int s = SA - 1;
-  for (; s + DW <= nk; s += DW)
-    static_for<0, DW>([&](auto j) { step(s + j, wv[(SA - 1 + j) % DW], std::integral_constant<int, WAIT>{}); });
-  static_for<0, DW>([&](auto j) {
-    if (s + j < nk) step(s + j, wv[(SA - 1 + j) % DW], std::integral_constant<int, WAIT>{});
-  });
-  LSD_STAMP(1)
-
-  // epilogue through LDS: every DMA landed (the tail re-stages included) and
-  // every wave's fragment reads retired before the C tile overwrites the ring
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-  __syncthreads();
-  constexpr int CLD = BN + 4;
-  float* ct = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ct[(i * 16 + 4 * g + q) * CLD + 16 * w + r] = acc[i][q];
-  __syncthreads();
-  ct_store<EPI, BN, BM, NWV * 64>(p, ct, m0, n0, split);
-  LSD_STAMP(2)
-}
+// Measured and removed this round: a decode GEMM that streams the weights
+// HBM -> VGPRs several k-steps ahead (A alone through an LDS ring; 4 or 8
+// waves, 64-128-row tiles).  Equal on GPT-2 XL QKV at 96-row tiles, 20-150 %
+// slower elsewhere: issue-bound with one wave per SIMD, 2x TA work from the
+// fragment-shaped weight loads (profiles/r5_vw_ab.log, r5_vw8_ab.log,
+// r5_pmc_decode_gemm.txt; code in git history, commit 78fca21 and after).
 
 // ---------------------------------------------------------------------------
 // Host launchers
@@ -2092,46 +1959,6 @@ static hipError_t launch_d256(const GemmParams& p, int kind, int* cnt, float* ws
   return bn == 128 ? launch_d256_bn<EPI, 128>(p, cnt, ws, st) : launch_d256_bn<EPI, 64>(p, cnt, ws, st);
 }
 
-// gemm_vw variant (lsd_gemm_set_vw): rows per tile (MT = 16-row MFMA tiles), W k-steps in
-// flight (DW), A ring slots (SA), waves (NWV: 64 or 128-column tiles)
-static int g_vw_mt = 8, g_vw_dw = 6, g_vw_sa = 4, g_vw_nw = 4;
-
-static bool vw_ok(int M, int N, int K) { return M >= 1 && M <= 256 && K % 64 == 0 && N % 64 == 0; }
-static int vw_tiles_m(int M) { return (M + 16 * g_vw_mt - 1) / (16 * g_vw_mt); }
-
-template <int EPI, int MT, int NWV>
-static hipError_t launch_vw_mt(const GemmParams& p, hipStream_t st) {
-  const int tm = (p.M + 16 * MT - 1) / (16 * MT), tn = (p.N + 16 * NWV - 1) / (16 * NWV);
-  const dim3 grid(tm * tn * p.splits), block(NWV * 64);
-#define LSD_VW(DW, SA)                                                                               \
-  if (g_vw_dw == DW && g_vw_sa == SA) {                                                              \
-    hipLaunchKernelGGL((gemm_vw_kernel<EPI, MT, DW, SA, NWV>), grid, block, 0, st, p, tm, tn);       \
-    return hipGetLastError();                                                                        \
-  }
-  LSD_VW(4, 3) LSD_VW(6, 4) LSD_VW(8, 4) LSD_VW(8, 6)
-#undef LSD_VW
-  return hipErrorInvalidValue;
-}
-
-template <int EPI>
-static hipError_t launch_vw(const GemmParams& p, hipStream_t st) {
-  if (!vw_ok(p.M, p.N, p.K) || (p.splits > 1 && EPI != EPI_SLAB)) return hipErrorInvalidValue;
-  if (g_vw_nw == 8) {
-    if (EPI == EPI_SILU_MUL && p.N % 128) return hipErrorInvalidValue;  // gate/up pairs inside a tile
-    switch (g_vw_mt) {
-      case 4: return launch_vw_mt<EPI, 4, 8>(p, st);
-      case 8: return launch_vw_mt<EPI, 8, 8>(p, st);
-      default: return hipErrorInvalidValue;
-    }
-  }
-  switch (g_vw_mt) {
-    case 4: return launch_vw_mt<EPI, 4, 4>(p, st);
-    case 6: return launch_vw_mt<EPI, 6, 4>(p, st);
-    case 8: return launch_vw_mt<EPI, 8, 4>(p, st);
-    default: return hipErrorInvalidValue;
-  }
-}
-
 template <int EPI>
 static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
   // 256x256 pipelined kernel once the problem fills the chip with 1-block/CU
@@ -2232,20 +2059,7 @@ extern "C" void lsd_gemm_set_ring8(int v) { g_ring8 = (v == 1 || v == 2) ? v : 0
 extern "C" void lsd_gemm_set_ring8_flags(int v) { g_ring8_flags = v & 7; }
 extern "C" void lsd_gemm_set_ring8_pack(int v) { g_ring8_pack = v & 3; }
 extern "C" void lsd_gemm_set_d256_slots(int v) { g_d256_slots = v < 2 ? 2 : (v > 4 ? 4 : v); }
-// gemm_vw variant: code = NWV * 1000 + MT * 100 + DW * 10 + SA (e.g. 4864: 4 waves, 128 rows,
-// 6 W steps, 4 A slots; 8464: 8 waves x 16 columns, 64 rows); a 3-digit code means 4 waves
-extern "C" int lsd_gemm_set_vw(int code) {
-  const int nw = code >= 1000 ? code / 1000 : 4, mt = code / 100 % 10, dw = code / 10 % 10, sa = code % 10;
-  const bool ok = (nw == 4 ? (mt == 4 || mt == 6 || mt == 8) : (nw == 8 && (mt == 4 || mt == 8))) &&
-                  ((dw == 4 && sa == 3) || (dw == 6 && sa == 4) || (dw == 8 && sa == 4) || (dw == 8 && sa == 6));
-  if (!ok) return -1;
-  g_vw_nw = nw;
-  g_vw_mt = mt;
-  g_vw_dw = dw;
-  g_vw_sa = sa;
-  return 0;
-}
-extern "C" int lsd_gemm_vw_tiles_m(int M) { return vw_tiles_m(M); }
+
 // columns per gemm_d256 tile of a launch of this kind (0: not a d256 launch):
 // the split workspace and ticket counters are sized from it (bindings.cpp)
 extern "C" int lsd_gemm_d256_bn(int kind, int M, int N, int K) { return d256_bn(kind, M, N, K); }
@@ -2275,9 +2089,8 @@ extern "C" hipError_t lsd_gemm(const GemmParams* p, int epi, int kind, int* cnt,
                                hipStream_t st) {
 #define LSD_DISPATCH(E)                                                                   \
   case E:                                                                                 \
-    return kind == 4 ? launch_vw<E>(*p, st)                                               \
-           : kind >= 2 ? launch_d256<E>(*p, kind, cnt, ws, st)                            \
-                       : (kind ? launch_tiled<E>(*p, cnt, ws, st) : launch_sk<E>(*p, cnt, ws, st));
+    return kind >= 2 ? launch_d256<E>(*p, kind, cnt, ws, st)                              \
+                     : (kind ? launch_tiled<E>(*p, cnt, ws, st) : launch_sk<E>(*p, cnt, ws, st));
   switch (epi) {
     LSD_DISPATCH(EPI_BF16)
     LSD_DISPATCH(EPI_GELU)

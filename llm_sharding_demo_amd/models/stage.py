@@ -71,8 +71,6 @@ class StageModel:
         # plain PyTorch ops (ops/reference.py) on the GPU (utils/golden.py)
         self.backend = backend if backend is not None else get_backend(self.device)
         self.backend.prepare_stage(self)
-        # callable(kv layer, before: bool) around each attention launch, or None
-        self.attn_gate = None
 
     def _owns(self, name: str) -> bool:
         """Is tensor `name` used by this stage (its units, embeddings, head)?"""
@@ -104,12 +102,7 @@ class StageModel:
         fused = getattr(be, "attention_oproj", None)
         if fused is not None and fused(q, self.kv.k(li), self.kv.v(li), meta, wo, bo, r):
             return
-        gate = self.attn_gate  # decode lanes' attention ordering (parallel/pipeline.py)
-        if gate is not None:
-            gate(li, True)
         o = be.attention(q, self.kv.k(li), self.kv.v(li), meta)
-        if gate is not None:
-            gate(li, False)
         be.linear_residual(o, wo, bo, r)
 
     def _gpt2_mlp(self, i: int, r: Residual) -> None:

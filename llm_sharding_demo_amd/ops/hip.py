@@ -127,9 +127,11 @@ class HipBackend(Backend):
     # microbatches: 41.2k vs 39.7k tok/s on the tiled kernel (GPT-2 XL, 2 x 256)
     SK_MAX_M = int(os.environ.get("LSD_SK_MAX_M", "256"))
     DEFER_RESID = os.environ.get("LSD_DEFER_RESID", "1") == "1"
-    # prefill residual projections: bf16 slab + fold in the next norm
-    # (LSD_PREFILL_SLAB=0: fp32 read-modify-write in the GEMM epilogue)
-    PREFILL_SLAB = os.environ.get("LSD_PREFILL_SLAB", "1") == "1"
+    # prefill residual projections as one bf16 slab folded by the next norm
+    # instead of the GEMM epilogue's fp32 read-modify-write of the residual:
+    # prefill 222.6 / 225.1 vs 224.5 / 225.8 ms on the headline, within noise
+    # (profiles/r5_prefill_slab_ab.log) -- opt-in (LSD_PREFILL_SLAB=1)
+    PREFILL_SLAB = os.environ.get("LSD_PREFILL_SLAB", "0") == "1"
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
     # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:

@@ -373,15 +373,6 @@ class StageWorker(racecheck.Shared):
         self._tev_used: List[torch.cuda.Event] = []
         self.native_steps = 0
         self.io_items = 0  # decode items whose (graph) body carried its own transfers
-        # LSD_LANE_ORDER=1: the decode attention launches of the lanes take
-        # turns -- lane l's attention of layer i waits for lane l-1's of layer
-        # i (lane 0: lane L-1's of layer i-1) through external event nodes in
-        # the captured graphs, so the HBM-bound attention of one group runs
-        # beside the other group's GEMMs instead of beside its attention
-        # (tools/lane_schedule_ab.py)
-        self.lane_order = (self.device.type == "cuda" and len(self.lanes) > 1
-                           and os.environ.get("LSD_LANE_ORDER", "0") == "1")
-        self._lane_ev: Dict[tuple, torch.cuda.Event] = {}
 
     # ------------------------------------------------------------------
     def configure(self, groups: int, cap: int) -> None:
@@ -820,12 +811,7 @@ class StageWorker(racecheck.Shared):
             if io and not self.first:  # the edge receive, inside the graph
                 self._recv(inp, self.r - 1, "fwd", lane, stage=gs.wire_buf(self, gp.b), capture=True)
             meta = gs.meta(gp.b, gp.ctxb)
-            if self.lane_order:
-                self.stage.attn_gate = lambda li, before: self._lane_gate(lane, li, before)
-            try:
-                out = self.stage.forward(meta, inp, head=True, variant=gp.g & 1)
-            finally:
-                self.stage.attn_gate = None
+            out = self.stage.forward(meta, inp, head=True, variant=gp.g & 1)
             if not self.last:
                 meta.advance()
                 if io:
@@ -855,24 +841,6 @@ class StageWorker(racecheck.Shared):
         self.captures += 1
         self._replay(gs, key, g)
         return out
-
-    def _lane_gate(self, lane: int, li: int, before: bool) -> None:
-        """LSD_LANE_ORDER: wait for the previous lane's attention of this
-        layer (lane 0: the last lane's of the layer before) / publish this
-        lane's.  External events, so the record / wait become graph nodes
-        that order separately launched graphs."""
-        L = len(self.lanes)
-        cur = torch.cuda.current_stream(self.device)
-        if before:
-            key = (lane - 1, li) if lane > 0 else (L - 1, li - 1)
-            ev = self._lane_ev.get(key)
-            if ev is not None:
-                cur.wait_event(ev)
-            return
-        ev = self._lane_ev.get((lane, li))
-        if ev is None:
-            ev = self._lane_ev[(lane, li)] = torch.cuda.Event(external=True)
-        ev.record(cur)
 
     def _replay(self, gs: GroupState, key: tuple, g) -> None:
         if getattr(self.t, "aborted", False):

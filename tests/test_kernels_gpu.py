@@ -364,50 +364,6 @@ def test_d256_gemm_epilogues(D256, CNT, M, K, splits):
     assert int(CNT.abs().sum()) == 0  # every ticket re-armed
 
 
-@pytest.fixture(params=[864, 884, 843, 886, 664, 684, 464, 8464, 8864, 8484, 8443])
-def VW(C, request):
-    """gemm_vw_kernel variants (launch kind 4): [NWV *1000 +] MT * 100 + DW * 10 + SA =
-    [8 waves x 16 columns,] 16-row tiles per workgroup, W k-steps in flight in
-    VGPRs, A ring slots."""
-    C.gemm_set_vw(request.param)
-    yield C
-    C.gemm_set_vw(864)
-
-
-@pytest.mark.parametrize("M", [1, 33, 100, 129, 200, 256])
-@pytest.mark.parametrize("K,splits", [(64, 1), (192, 1), (384, 3), (640, 2), (1600, 1), (1600, 5)])
-def test_vw_gemm_epilogues(VW, CNT, M, K, splits):
-    """W-to-VGPR decode kernel: every epilogue, row tails, 1 to 25 k-steps
-    (fewer than the W / A ring depths included), K splits into residual
-    slabs folded by the norm."""
-    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
-
-    C = VW
-    N = 320
-    a, w, bias = bf(M, K, seed=90), bf(N, K, scale=0.05, seed=91), bf(N, scale=0.1, seed=92)
-    y_ref = ref.linear(a, w, bias)
-    if splits == 1:
-        for _ in range(2):
-            close(C.linear(a, w, bias, 0, 4, 1, CNT), y_ref, 3e-2)
-        close(C.linear(a, w, bias, 1, 4, 1, CNT), ref.gelu_new(y_ref), 3e-2)
-        w2 = w[:256].contiguous()
-        y = C.linear(a, interleave_gate_up(w2, 128).contiguous(), None, 2, 4, 1, CNT)
-        close(y, ref.silu_mul(*ref.linear(a, w2).split(128, 1)), 3e-2)
-        close(C.linear_f32(a, w, 4, 1, CNT), ref.linear(a, w), 2e-3, 1e-3)
-    else:
-        with pytest.raises(RuntimeError):  # no in-kernel combine: residual slabs only
-            C.linear(a, w, bias, 0, 4, splits, CNT)
-    x = torch.randn(M, N, device=DEV)
-    x_ref = x + y_ref
-    slab = C.linear_residual(a, w, bias, x, splits, 4, CNT, False)
-    if splits > 1:
-        assert slab is not None and slab.shape == (splits, M, N)
-        C.norm(x, slab, bias, None, None, 0.0, True, None, False)
-    else:
-        assert slab is None
-    close(x, x_ref, 2e-3, 1e-3)
-
-
 @pytest.fixture
 def BIG(C):
     """Force the pipelined 256x256 kernel for every tiled launch with M >= 256."""
@@ -482,21 +438,19 @@ def _cache(slots, n_kv, S, hd):
 
 
 @pytest.mark.parametrize("rope", [False, True])
-@pytest.mark.parametrize("mode", ["decode1", "decode4", "tiled", "big", "d256", "d256s3", "vw"])
+@pytest.mark.parametrize("mode", ["decode1", "decode4", "tiled", "big", "d256", "d256s3"])
 def test_qkv_kv_append(C, CNT, rope, mode):
     from llm_sharding_demo_amd.ops.hip import rope_pair_permutation, rope_table
 
     nh, n_kv, hd, H = 4, 2, 64, 256
     qs, kvs = nh * hd, n_kv * hd
-    tiled = mode in ("tiled", "big", "d256", "d256s3", "vw")
+    tiled = mode in ("tiled", "big", "d256", "d256s3")
     splits = 4 if mode == "decode4" else (3 if mode == "d256s3" else 1)
     # decode: 10 tokens of 2 sequences; tiled: 2 sequences of 150 tokens;
     # d256: 200 decode-like rows (100 + 100) on the 256-row kernel (kind 2)
     n0, n1 = (4, 6) if not tiled else ((100, 100) if mode.startswith("d256") else (150, 150))
     if mode.startswith("d256"):
         tiled = 2
-    if mode == "vw":  # 2 sequences x 100 decode-like rows on the W-to-VGPR kernel (kind 4)
-        n0, n1, tiled = 100, 100, 4
     T, slots, S = n0 + n1, 3, 320
     a, w, bias = bf(T, H, seed=13), bf(qs + 2 * kvs, H, scale=0.05, seed=14), bf(qs + 2 * kvs, scale=0.1, seed=15)
     tslot = torch.tensor([0] * n0 + [2] * n1, dtype=torch.int32, device=DEV)

@@ -91,14 +91,10 @@ def main():
                 x = x0.clone()
 
                 kind = 3 if bn == 128 else 2
-                if bn >= 1000:  # W-to-VGPR kernel (kind 4), bn = 1000 + variant code
-                    kind, vw = 4, bn - 1000
 
                 def run():
                     C.gemm_set_ring8(r8 & 15)  # read at launch (capture) time
                     C.gemm_set_ring8_flags(r8 >> 4)
-                    if kind == 4:
-                        C.gemm_set_vw(vw)
                     w = ws[it[0] % nw]
                     it[0] += 1
                     if resid:
@@ -121,12 +117,6 @@ def main():
 
             cases = [("ring", 0, 1, int(os.environ.get("D256_BASE_R8", "0")))]
             for v in variants:
-                if v.startswith("vw:"):  # vw:CODE[:S] -- S K splits for the residual shapes
-                    f = [int(x) for x in v[3:].split(":")]
-                    S = f[1] if len(f) > 1 else 1
-                    if S == 1 or resid:
-                        cases.append((f"vw{f[0]}s{S}", 1000 + f[0], S, 0))
-                    continue
                 if v.startswith("r8s:"):  # 8-wave ring, S K splits + in-kernel combine
                     C.gemm_set_ring8(2)
                     if not resid and C.gemm_ring8_tiles(M, N, K, int(v[4:])):

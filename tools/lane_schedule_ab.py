@@ -11,7 +11,12 @@ dependencies:
             the other lane's GEMMs only;
   serial -- one stream (no overlap at all).
 Prints one JSON line per mode: ms per decode step (both groups), median of
-interleaved rounds.  Weights: random init; KV context fixed at CTX positions."""
+interleaved rounds.  Weights: random init; KV context fixed at CTX positions.
+Round 5 (profiles/r5_lane_schedule.log): free 8.40 ms (graph) / 8.36 (eager),
+alternating attentions 8.77 (eager), one stream 10.53 -- the free overlap
+already beats enforced anti-phase; kept free.  (External event nodes, which
+would order two separately launched per-lane graphs, are disallowed by the
+ROCm build of torch.)"""
 from __future__ import annotations
 
 import json
@@ -30,11 +35,13 @@ from llm_sharding_demo_amd.runtime.batch import BatchMeta  # noqa: E402
 MODEL = os.environ.get("LANE_MODEL", "gpt2-xl")
 ROWS = int(os.environ.get("LANE_ROWS", "256"))
 CTX = int(os.environ.get("LANE_CTX", "192"))
-MODES = os.environ.get("LANE_MODES", "free,alt,serial").split(",")
+# hipGraph-replayed, or issued eagerly (-eager)
+MODES = os.environ.get("LANE_MODES", "free,free-eager,alt-eager,alt,serial").split(",")
 
 
 def main():
     dev = torch.device("cuda")
+    print("building the stage", flush=True)
     mc = get_model_config(MODEL)
     L = mc.n_layers
     st = StageModel(mc, 0, L, True, True, device=dev, dtype=torch.bfloat16, max_slots=2 * ROWS + 2,
@@ -50,11 +57,13 @@ def main():
         if mode == "serial":
             streams = [streams[0], streams[0]]
         done = {}  # (lane, layer) -> event recorded after that lane's attention
+        keep = []  # every event stays alive: an event destroyed mid-capture (a replaced
+        # dict entry) crashed hipStreamEndCapture (round-5 log)
 
         def lane_attention(g, li):
             def att(q, kc, vc, meta):
                 cur = torch.cuda.current_stream()
-                if mode == "alt":
+                if mode.startswith("alt"):
                     prev = done.get((1 - g, li)) if g == 1 else done.get((1, li - 1))
                     if prev is not None:
                         cur.wait_event(prev)
@@ -62,6 +71,7 @@ def main():
                 ev = torch.cuda.Event()
                 ev.record(cur)
                 done[(g, li)] = ev
+                keep.append(ev)
                 return o
             return att
 
@@ -98,22 +108,30 @@ def main():
             step()  # warm-up (workspace allocations)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        if mode.endswith("-eager"):
+            # eager issue: the host issues the ~670 launches of a step well
+            # inside its ~8 ms of GPU time
+            return step
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             step()
-        return g
+        return g.replay
 
-    graphs = {m: capture(m) for m in MODES}
-    for g in graphs.values():
-        g.replay()
+    print("stage built; capturing", flush=True)
+    runs = {}
+    for m in MODES:
+        runs[m] = capture(m)
+        print("ready", m, flush=True)
+    for r in runs.values():
+        r()
     torch.cuda.synchronize()
     times = {m: [] for m in MODES}
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(7):
-        for m, g in graphs.items():
+        for m, r in runs.items():
             s.record()
             for _ in range(5):
-                g.replay()
+                r()
             e.record()
             torch.cuda.synchronize()
             times[m].append(s.elapsed_time(e) / 5)

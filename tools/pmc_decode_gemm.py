@@ -1,7 +1,8 @@
 """A short program for rocprofv3 --pmc passes over ONE decode GEMM variant at
 256 rows (GPT-2 XL QKV shape by default): 20 launches over rotating weights
 (cold, like the model's weight stream).
-usage: pmc_decode_gemm.py CASE [N K]   CASE = ring8 | ring | vw<code> (gemm_vw variant)"""
+usage: pmc_decode_gemm.py CASE [N K]   CASE = ring8 | ring
+(the round-5 passes also ran the W-to-VGPR kernel, since removed: git history)"""
 import os
 import sys
 
@@ -21,9 +22,6 @@ b = torch.randn(N, device="cuda").bfloat16()
 kind = 1
 if case == "ring":
     C.gemm_set_ring8(0)
-elif case.startswith("vw"):
-    C.gemm_set_vw(int(case[2:]))
-    kind = 4
 for i in range(20):
     C.linear(a, ws[i % len(ws)], b, 0, kind, 1, None)
 torch.cuda.synchronize()
