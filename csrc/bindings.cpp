@@ -239,7 +239,7 @@ c10::optional<torch::Tensor> linear_residual(torch::Tensor a, torch::Tensor w,
               "residual x must be contiguous [M, N]");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "residual x must be 16-byte aligned");
   if (p.M == 0) return c10::nullopt;
-  if ((tiled || defer) && (splits > 1 || defer)) {
+  if ((tiled || defer) && (splits > 1 || (defer && tiled))) {
     // bf16 partial slabs (LSD_SLAB_BF16=0: fp32): half the bytes the GEMM
     // writes and the next norm reads, each partial rounded once to bf16 --
     // the precision of a bf16 GEMM output, folded into the fp32 residual.
