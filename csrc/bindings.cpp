@@ -31,7 +31,6 @@ void lsd_gemm_set_ring8(int v);
 void lsd_gemm_set_ring8_flags(int v);
 void lsd_gemm_set_ring8_pack(int v);
 int lsd_gemm_d256_bn(int kind, int M, int N, int K);
-void lsd_gemm_set_ring8_pf(int v);
 int lsd_gemm_ring8_tiles(int M, int N, int K, int S);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
@@ -679,8 +678,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("gemm_set_ring8_flags", [](int64_t v) { lsd_gemm_set_ring8_flags((int)v); });
   m.def("gemm_set_ring8_pack", [](int64_t v) { lsd_gemm_set_ring8_pack((int)v); });
-  // 8-wave ring: weight-line prefetch distance in k-steps (0 off; 2 / 4 / 6)
-  m.def("gemm_set_ring8_pf", [](int64_t v) { lsd_gemm_set_ring8_pf((int)v); });
   m.def("gemm_d256_bn", [](int64_t kind, int64_t M, int64_t N, int64_t K) {
     return lsd_gemm_d256_bn((int)kind, (int)M, (int)N, (int)K);
   });

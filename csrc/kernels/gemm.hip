@@ -953,14 +953,10 @@ __device__ __forceinline__ void stage_rows_packed(char* lds_tile, const bf16* sr
 // reloads the other partials (sc1 loads) and sums all S in split order
 // (deterministic) before the fused epilogue (guide §5 "In-launch split-K
 // reduction", sc1 form: no release / acquire fences).
-// PF > 0 (weight prefetch): with each k-step's loads every loading wave also
-// issues one 4-byte-per-lane LDS-DMA "touch" of the W lines PF k-steps past
-// the ring's look-ahead (its tile rows 8 per wave, one 128-B line each, into
-// a dummy 256-B LDS area) -- the lines reach the XCD's L2 before the ring
-// stages them, hiding the weight stream's HBM-miss latency (the cold-vs-warm
-// gap of profiles/r5_decode_gemm_cold_warm.log).  Counted like a load of the
-// step: the counted waits use LPS + 1.
-template <int EPI, int VAR, int SLOTS, int NTW = 0, int PK = 0, bool BL = kStageBL, int PF = 0>
+// Measured and removed (round 5): a W-line L2 prefetch, one extra 4-byte-per-lane
+// LDS-DMA touch per k-step of the rows 2-6 k-steps ahead -- 7-16 % slower on every
+// GPT-2 XL shape, bench 50.1-50.5k -> 46.5-47.3k (profiles/r5_rejected_ring8_prefetch.log).
+template <int EPI, int VAR, int SLOTS, int NTW = 0, int PK = 0, bool BL = kStageBL>
 __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles_m, int tiles_n, int rot,
                                                          int* __restrict__ cnt, float* __restrict__ ws) {
   constexpr int D = SLOTS - 1, TN = 64, TM = TBM;
@@ -970,10 +966,9 @@ __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles
   constexpr int JT = 2;                          // 16-column MFMA tiles per computing wave (32 cols)
   constexpr int A_BYTES = TM * TBK * 2;
   constexpr int SLOT_BYTES = A_BYTES + TN * TBK * 2;
-  constexpr int LPS = (TM + TN) / 8 / LWN + (PF > 0 ? 1 : 0);  // VMEM per loading wave per k-step: 6 / 3 (+1)
+  constexpr int LPS = (TM + TN) / 8 / LWN;      // glds per loading wave per k-step: 6 / 3
   constexpr int CLD = TN + 4;
-  constexpr int SMEM0 = SLOTS * SLOT_BYTES > TM * CLD * 4 ? SLOTS * SLOT_BYTES : TM * CLD * 4;
-  constexpr int SMEM = SMEM0 + (PF > 0 ? 256 : 0);  // + the touch loads' dummy LDS area
+  constexpr int SMEM = SLOTS * SLOT_BYTES > TM * CLD * 4 ? SLOTS * SLOT_BYTES : TM * CLD * 4;
   static_assert(VAR == 1 || VAR == 2, "ring8 layout");
   static_assert(SLOTS >= 3 && SLOTS <= 5 && (SLOTS - 2) * LPS <= 63, "ring depth / vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];  // [slot][A|W]; then the C tile
@@ -1009,14 +1004,6 @@ __global__ __launch_bounds__(512) void gemm_ring8_kernel(GemmParams p, int tiles
     else stage_rows<TM, LWN, 0, BL>(b, p.A, p.lda, m0, p.M - 1, k * TBK, lw);
     if constexpr (PK & 1) stage_rows_packed<TN, LWN, 1>(b + A_BYTES, p.W, p.N, p.K / 64, n0, p.N - 1, k, lw);
     else stage_rows<TN, LWN, NTW ? 2 : 0, BL>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, k * TBK, lw);
-    if constexpr (PF > 0) {
-      // touch: rows n0 + 8 lw + (lane & 7), the 128-B line of k-step kt + PF
-      // (clamped into the split: re-touching an L2-hot line is cheap)
-      const int kp = min(k + PF, ke - 1);
-      const int row = min(n0 + (TN / LWN) * lw + (lane & 7), p.N - 1);
-      __builtin_amdgcn_global_load_lds((gbl_cvoid*)(p.W + (long)row * p.ldw + (long)kp * TBK),
-                                       (lds_void*)(smem + SMEM0), 4, 0, 0);
-    }
   };
   if (loader) {
 #pragma unroll
@@ -1885,9 +1872,6 @@ static int g_ring8_flags = 0;
 // lsd_gemm_set_ring8_pack(): operands in k-block-packed layouts (bit 0 W, bit 1 A; A/B only)
 static int g_ring8_pack = 0;
 static int g_d256_slots = 3;  // lsd_gemm_set_d256_slots(): gemm_d256 ring depth 2..4 (BN 128: at most 3)
-// lsd_gemm_set_ring8_pf(): weight-line prefetch distance of the 8-wave ring (k-steps past its
-// look-ahead; 0 = off, 2 / 4 / 6)
-static int g_ring8_pf = 0;
 // Decode GEMM row blocking: when the column tiles x K splits leave the chip
 // under-filled (< g_rb_fill workgroups, e.g. the deferred-residual projections
 // with N = H), M > g_sk_rows rows run as ceil(M / g_sk_rows) row blocks
@@ -2040,12 +2024,6 @@ static hipError_t launch_tiled(const GemmParams& p, int* cnt, float* ws, hipStre
         hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 0, true>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else if (g_ring8 == 2 && (g_ring8_flags & 2))
         hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 1>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
-      else if (g_ring8 == 2 && g_ring8_pf == 2)
-        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 0, kStageBL, 2>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
-      else if (g_ring8 == 2 && g_ring8_pf == 4)
-        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 0, kStageBL, 4>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
-      else if (g_ring8 == 2 && g_ring8_pf == 6)
-        hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3, 0, 0, kStageBL, 6>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else if (g_ring8 == 2)
         hipLaunchKernelGGL((gemm_ring8_kernel<EPI, 2, 3>), g8, b8, 0, st, p, tm, tn64, rot, cnt, ws);
       else
@@ -2084,7 +2062,6 @@ extern "C" void lsd_gemm_set_ring8(int v) { g_ring8 = (v == 1 || v == 2) ? v : 0
 extern "C" void lsd_gemm_set_ring8_flags(int v) { g_ring8_flags = v & 7; }
 extern "C" void lsd_gemm_set_ring8_pack(int v) { g_ring8_pack = v & 3; }
 extern "C" void lsd_gemm_set_d256_slots(int v) { g_d256_slots = v < 2 ? 2 : (v > 4 ? 4 : v); }
-extern "C" void lsd_gemm_set_ring8_pf(int v) { g_ring8_pf = (v == 2 || v == 4 || v == 6) ? v : 0; }
 
 // columns per gemm_d256 tile of a launch of this kind (0: not a d256 launch):
 // the split workspace and ticket counters are sized from it (bindings.cpp)

@@ -210,8 +210,6 @@ class HipBackend(Backend):
     # (p50 8.72 ms: 96 KiB of LDS per workgroup), so 3 slots.
     RING8 = int(os.environ.get("LSD_RING8", "2"))
     RING8_FLAGS = int(os.environ.get("LSD_RING8_FLAGS", "0"))  # A/B bits (gemm.hip)
-    # 8-wave ring weight-line prefetch distance (k-steps; 0 = off), gemm.hip gemm_ring8_kernel PF
-    RING8_PF = int(os.environ.get("LSD_RING8_PF", "0"))
     # K splits of the non-residual decode GEMMs on the 8-wave ring (QKV, MLP-up,
     # 129-256 rows) with the in-kernel last-arriver combine: aim at this many
     # workgroups (0 = off: one workgroup per 128x64 tile)
@@ -229,7 +227,6 @@ class HipBackend(Backend):
         self.C.gemm_set_d256_slots(self.D256_SLOTS)
         self.C.gemm_set_ring8(self.RING8)
         self.C.gemm_set_ring8_flags(self.RING8_FLAGS)
-        self.C.gemm_set_ring8_pf(self.RING8_PF)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))

@@ -270,22 +270,19 @@ def test_ring_gemm_96_row_tiles(C, CNT, M, K):
         C.gemm_set_ring_tn(128)
 
 
-@pytest.fixture(params=[(1, 0, 0), (2, 0, 0), (2, 1, 0), (2, 2, 0), (2, 0, 2), (2, 0, 6)])
+@pytest.fixture(params=[(1, 0), (2, 0), (2, 1), (2, 2)])
 def RING8(C, request):
-    """128x64 decode ring on 8 waves (gemm_ring8_kernel): (layout, A/B flags,
-    weight prefetch distance) -- 1 = 4 computing + 4 loader waves, 2 = 8
-    computing waves; flag 1 = rotated K start per tile, 2 = nt weight
-    staging; prefetch N = 4-byte LDS-DMA touch of each W row N k-steps ahead."""
-    var, flags, pf = request.param
+    """128x64 decode ring on 8 waves (gemm_ring8_kernel): (layout, A/B flags)
+    -- 1 = 4 computing + 4 loader waves, 2 = 8 computing waves; flag 1 =
+    rotated K start per tile, 2 = nt weight staging."""
+    var, flags = request.param
     C.gemm_set_tiled3_max(1 << 30)
     C.gemm_set_ring_tn(64)
     C.gemm_set_ring8(var)
     C.gemm_set_ring8_flags(flags)
-    C.gemm_set_ring8_pf(pf)
     yield C, var
     C.gemm_set_ring8(0)
     C.gemm_set_ring8_flags(0)
-    C.gemm_set_ring8_pf(0)
     C.gemm_set_tiled3_max(0)
     C.gemm_set_ring_tn(128)
 

@@ -95,7 +95,6 @@ def main():
                 def run():
                     C.gemm_set_ring8(r8 & 15)  # read at launch (capture) time
                     C.gemm_set_ring8_flags((r8 >> 4) & 15)
-                    C.gemm_set_ring8_pf(r8 >> 8)
                     w = ws[it[0] % nw]
                     it[0] += 1
                     if resid:
@@ -118,9 +117,6 @@ def main():
 
             cases = [("ring", 0, 1, int(os.environ.get("D256_BASE_R8", "0")))]
             for v in variants:
-                if v.startswith("pf:"):  # 8-wave ring with weight-line prefetch, distance N k-steps
-                    cases.append((f"ring8pf{v[3:]}", 0, 1, 2 + (int(v[3:]) << 8)))
-                    continue
                 if v.startswith("r8s:"):  # 8-wave ring, S K splits + in-kernel combine
                     C.gemm_set_ring8(2)
                     if not resid and C.gemm_ring8_tiles(M, N, K, int(v[4:])):
@@ -146,7 +142,6 @@ def main():
             diffs = [float((o - base).abs().max()) for o in outs]
             times = graph_time([make(bn, S, r8) for _, bn, S, r8 in cases])
             C.gemm_set_ring8(0)
-            C.gemm_set_ring8_pf(0)
             for (lab, bn, S, _), t, d in zip(cases, times, diffs):
                 row = {"M": M, "shape": name, "N": N, "K": K, "case": lab,
                        "us_med": round(statistics.median(t), 2), "us_min": round(min(t), 2),
