@@ -64,7 +64,7 @@ hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st)
 hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                       const int* topk, const int* greedy, const long long* seeds,
                       long long* step, int* out, int advance, const int* active, int* pos,
-                      hipStream_t st);
+                      const float* segmax, long ldseg, hipStream_t st);
 }
 
 namespace {
@@ -213,11 +213,21 @@ torch::Tensor linear(torch::Tensor a, torch::Tensor w, c10::optional<torch::Tens
   return out;
 }
 
-// fp32 logits = a @ w^T
+// fp32 logits = a @ w^T.  segmax (tiled kernels only): also the max of every
+// 8-column segment, fp32 [M, N / 8] -- the sampler then reads the logits only
+// in the segments that can hold a top-k element (sample.hip)
 torch::Tensor linear_f32(torch::Tensor a, torch::Tensor w, int64_t tiled, int64_t splits,
-                         c10::optional<torch::Tensor> counters) {
+                         c10::optional<torch::Tensor> counters, c10::optional<torch::Tensor> segmax) {
   GemmParams p = base_params(a, w, tiled);
   auto out = torch::empty({p.M, p.N}, a.options().dtype(torch::kFloat32));
+  if (segmax.has_value()) {
+    TORCH_CHECK(tiled != 0, "linear_f32: segment maxima need a tiled kernel");
+    need(*segmax, torch::kFloat32, "segmax");
+    TORCH_CHECK(segmax->dim() == 2 && segmax->is_contiguous() && segmax->size(0) == p.M &&
+                segmax->size(1) == p.N / 8, "segmax must be contiguous fp32 [M, N / 8]");
+    p.segmax = segmax->data_ptr<float>();
+    p.ldseg = p.N / 8;
+  }
   if (p.M == 0) return out;
   p.out = out.data_ptr(); p.ldo = p.N;
   run_gemm(p, EPI_F32, tiled, splits, counters, a, "linear_f32");
@@ -577,7 +587,8 @@ void sample_launch(const torch::Tensor& logits, int64_t V, const torch::Tensor& 
                    const torch::Tensor& topk, const torch::Tensor& greedy, const torch::Tensor& seeds,
                    torch::Tensor& step, torch::Tensor& out, bool advance,
                    const c10::optional<torch::Tensor>& active = c10::nullopt,
-                   const c10::optional<torch::Tensor>& pos = c10::nullopt) {
+                   const c10::optional<torch::Tensor>& pos = c10::nullopt,
+                   const c10::optional<torch::Tensor>& segmax = c10::nullopt) {
   need(logits, torch::kFloat32, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && V <= logits.size(1) && V >= 1, "logits [B, >=V]");
   TORCH_CHECK(logits.stride(0) % 4 == 0 && logits.size(1) % 4 == 0, "logits row length must be a multiple of 4");
@@ -605,17 +616,28 @@ void sample_launch(const torch::Tensor& logits, int64_t V, const torch::Tensor& 
     TORCH_CHECK(pos->numel() == B && pos->is_contiguous(), "pos must be contiguous int32 [B]");
     pp = pos->data_ptr<int>();
   }
+  const float* sm = nullptr;
+  long ldseg = 0;
+  if (segmax.has_value()) {  // linear_f32's segment maxima of these logits
+    need(*segmax, torch::kFloat32, "segmax");
+    TORCH_CHECK(segmax->dim() == 2 && segmax->is_contiguous() && segmax->size(0) == B &&
+                logits.size(1) % 8 == 0 && segmax->size(1) == logits.size(1) / 8,
+                "segmax must be contiguous fp32 [B, logits row length / 8]");
+    sm = segmax->data_ptr<float>();
+    ldseg = segmax->size(1);
+  }
   check_hip(lsd_sample(logits.data_ptr<float>(), logits.stride(0), B, V, temp.data_ptr<float>(),
                        topk.data_ptr<int>(), greedy.data_ptr<int>(),
                        reinterpret_cast<const long long*>(seeds.data_ptr<int64_t>()),
                        reinterpret_cast<long long*>(step.data_ptr<int64_t>()),
-                       out.data_ptr<int>(), advance ? 1 : 0, act, pp, cur_stream()), "sample");
+                       out.data_ptr<int>(), advance ? 1 : 0, act, pp, sm, ldseg, cur_stream()), "sample");
 }
 
 torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
-                     torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step) {
+                     torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step,
+                     c10::optional<torch::Tensor> segmax) {
   auto out = torch::empty({logits.size(0)}, logits.options().dtype(torch::kInt32));
-  sample_launch(logits, V, temp, topk, greedy, seeds, step, out, false);
+  sample_launch(logits, V, temp, topk, greedy, seeds, step, out, false, c10::nullopt, c10::nullopt, segmax);
   return out;
 }
 
@@ -625,8 +647,9 @@ torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch:
 // in the same kernel.
 void sample_into(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
                  torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step, torch::Tensor out,
-                 c10::optional<torch::Tensor> active, c10::optional<torch::Tensor> pos) {
-  sample_launch(logits, V, temp, topk, greedy, seeds, step, out, true, active, pos);
+                 c10::optional<torch::Tensor> active, c10::optional<torch::Tensor> pos,
+                 c10::optional<torch::Tensor> segmax) {
+  sample_launch(logits, V, temp, topk, greedy, seeds, step, out, true, active, pos, segmax);
 }
 
 }  // namespace
@@ -641,7 +664,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   lsd_register_exec(m);
   lsd_register_loopback(m);
   m.def("linear", &linear);
-  m.def("linear_f32", &linear_f32);
+  m.def("linear_f32", &linear_f32, py::arg("a"), py::arg("w"), py::arg("tiled"), py::arg("splits"),
+        py::arg("counters"), py::arg("segmax") = py::none());
   m.def("linear_residual", &linear_residual);
   m.def("linear_qkv", &linear_qkv);
   m.def("embed", &embed);
@@ -649,10 +673,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_decode", &attn_decode);
   m.def("attn_prefill", &attn_prefill);
   m.def("attn_oproj", &attn_oproj);
-  m.def("sample", &sample);
+  m.def("sample", &sample, py::arg("logits"), py::arg("V"), py::arg("temp"), py::arg("topk"),
+        py::arg("greedy"), py::arg("seeds"), py::arg("step"), py::arg("segmax") = py::none());
   m.def("sample_into", &sample_into, py::arg("logits"), py::arg("V"), py::arg("temp"), py::arg("topk"),
         py::arg("greedy"), py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("active"),
-        py::arg("pos") = py::none());
+        py::arg("pos") = py::none(), py::arg("segmax") = py::none());
   m.def("gemv", &gemv);
   // GEMV weight stream with non-temporal loads (A/B knob, LSD_GEMV_NT)
   m.def("gemv_set_nt", [](int64_t v) { lsd_gemv_set_nt((int)v); });

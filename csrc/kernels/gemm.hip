@@ -196,6 +196,14 @@ __device__ __forceinline__ void epi8_post(const GemmParams& p, int m, int n, con
                                : reinterpret_cast<float*>(p.out) + (long)m * p.ldo + n;
     reinterpret_cast<f32x4*>(o)[0] = f32x4{v[0], v[1], v[2], v[3]};
     reinterpret_cast<f32x4*>(o)[1] = f32x4{v[4], v[5], v[6], v[7]};
+    if constexpr (EPI == EPI_F32) {
+      // lm_head: the chunk's maximum for the sampler (one float per 8 logits)
+      if (p.segmax) {
+        const float m01 = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        const float m23 = fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7]));
+        p.segmax[(long)m * p.ldseg + (n >> 3)] = fmaxf(m01, m23);
+      }
+    }
     return;
   }
   float y[8];

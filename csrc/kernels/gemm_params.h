@@ -24,6 +24,9 @@ struct GemmParams {
   const float* rope;  // [max_pos][hd/2][2] (cos, sin), or null
   long long* stamps;  // diagnostic builds only: per-workgroup s_memrealtime phase stamps
   int slab_bf16;      // EPI_SLAB: partial slabs stored bf16 instead of fp32 (LSD_SLAB_BF16)
+  // EPI_F32 (tiled kernels): also the max of every 8-column segment,
+  // segmax[m * ldseg + n / 8] -- the sampler's first pass, fused (sample.hip)
+  float* segmax; long ldseg;
 };
 
 // Small-M (M <= 8) weight-streaming GEMV with an optional fused input norm

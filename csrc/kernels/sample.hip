@@ -22,6 +22,11 @@
 //           u = splitmix64(seed * FNV + step) -- the same counter-based
 //           generator as runtime/batch.py:counter_uniform, so a seeded
 //           request reproduces across batch layouts and stage counts.
+//   top-k <= 64 with segment maxima (lm_head's epilogue wrote the max of
+//           every 8-logit segment, gemm.hip epi8_post): the threshold comes
+//           from the segment maxima (25 KB per GPT-2 row instead of 200 KB)
+//           and only the segments whose maximum reaches it are read -- the
+//           same candidate superset rule, so the same draws.
 #include "common.h"
 
 namespace lsd {
@@ -102,6 +107,50 @@ __device__ __forceinline__ void advance_row(long long* step, int* pos, const int
   if (pos) pos[row] += a;
 }
 
+// k-th largest of the 64 16-thread group maxima of mx (ties by group): with
+// every group maximum an element of the row (or -inf), a lower bound of the
+// row's k-th largest element -- the top-k group maxima are k distinct
+// elements >= it.  Two block barriers.
+__device__ __forceinline__ float kth_group_max(float mx, int k, float* cval, float* redv) {
+  const int tid = threadIdx.x;
+  mx = fmaxf(mx, wave_xchg<1>(mx));
+  mx = fmaxf(mx, wave_xchg<2>(mx));
+  mx = fmaxf(mx, wave_xchg<4>(mx));
+  mx = fmaxf(mx, wave_xchg<8>(mx));
+  if ((tid & 15) == 0) cval[tid >> 4] = mx;
+  __syncthreads();
+  if (tid < 64) {  // rank of group `tid` among the 64 maxima
+    const float sv = cval[tid];
+    int rank = 0;
+#pragma unroll
+    for (int j4 = 0; j4 < 16; ++j4) {
+      const f32x4 o = reinterpret_cast<const f32x4*>(cval)[j4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rank += (o[e] > sv || (o[e] == sv && 4 * j4 + e < tid)) ? 1 : 0;
+    }
+    if (rank == k - 1) redv[0] = sv;
+  }
+  __syncthreads();
+  return redv[0];
+}
+
+// Block-wide slot assignment for `cnt` entries of this thread: wave-inclusive
+// scan, one LDS atomic per wave on `s_cnt`; returns the thread's first slot.
+__device__ __forceinline__ unsigned claim_slots(int cnt, unsigned* s_cnt) {
+  const int lane = lane_id();
+  int incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  unsigned base = 0;
+  if (lane == 63) base = atomicAdd(s_cnt, (unsigned)incl);
+  return __shfl(base, 63, 64) + (unsigned)(incl - cnt);
+}
+
+constexpr int SCH = 16;  // segment maxima per thread: rows of <= SCH * NT * 8 logits
+
 __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ logits, long ld,
                                                     int V, const float* __restrict__ temp,
                                                     const int* __restrict__ topk,
@@ -110,7 +159,8 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
                                                     long long* __restrict__ step,
                                                     int* __restrict__ out, int advance,
                                                     const int* __restrict__ active,
-                                                    int* __restrict__ pos) {
+                                                    int* __restrict__ pos,
+                                                    const float* __restrict__ segmax, long ldseg) {
   __shared__ unsigned hist[4096];
   __shared__ float cval[SMAX];
   __shared__ int cidx[SMAX];
@@ -160,7 +210,74 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
   // asc) order comes from the bitonic sort below, so the result equals the
   // radix path's.  More than SMAX candidates (flat logits) -> radix path.
   bool fast = k <= 64;
-  if (fast) {
+  const int S = (V + 7) >> 3;  // 8-logit segments holding real logits (the last may be partial)
+  if (fast && segmax != nullptr && S <= SCH * NT) {
+    // ---- segment-maxima path: tau from the lm_head epilogue's segment
+    // maxima; a segment whose maximum is below tau holds no candidate, so only
+    // the others are read.  The last segment, when partial, also covers padded
+    // vocabulary columns: its maximum is taken over the real logits only.
+    const float* sm = segmax + (long)row * ldseg;
+    const int Sfull = V >> 3, nch = (S + NT - 1) / NT;
+    float q[SCH];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < SCH; ++i)
+      if (i < nch) q[i] = sm[min(tid + i * NT, S - 1)];
+#pragma unroll
+    for (int i = 0; i < SCH; ++i) {
+      if (i >= nch) break;
+      const int sg = tid + i * NT;
+      if (sg >= S) q[i] = -INFINITY;
+      if (sg == Sfull && Sfull < S) {
+        float pm = -INFINITY;
+        for (int j = 8 * sg; j < V; ++j) pm = fmaxf(pm, x[j]);
+        q[i] = pm;
+      }
+      mx = fmaxf(mx, q[i]);
+    }
+    if (tid == 0) s_cnt = 0;
+    const float tau = kth_group_max(mx, k, cval, redv);
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < SCH; ++i) {
+      if (i >= nch) break;
+      if (q[i] >= tau) {  // -inf segments (past S) never pass unless tau is -inf
+        const int sg = tid + i * NT;
+        if (sg < S) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(x + 8 * sg);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(x + 8 * sg + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            cnt += (a[j] >= tau && 8 * sg + j < V) ? 1 : 0;
+            cnt += (b[j] >= tau && 8 * sg + 4 + j < V) ? 1 : 0;
+          }
+        }
+      }
+    }
+    unsigned slot = claim_slots(cnt, &s_cnt);
+#pragma unroll
+    for (int i = 0; i < SCH; ++i) {
+      if (i >= nch) break;
+      const int sg = tid + i * NT;
+      if (q[i] >= tau && sg < S) {  // the segment's 32 bytes again, from L1 / L2
+        const f32x4 a = *reinterpret_cast<const f32x4*>(x + 8 * sg);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(x + 8 * sg + 4);
+        const float v8[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (v8[j] >= tau && 8 * sg + j < V) {
+            if (slot < SMAX) {
+              cval[slot] = v8[j];
+              cidx[slot] = 8 * sg + j;
+            }
+            ++slot;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    fast = s_cnt <= SMAX;  // uniform; more -> radix path over the full row
+  } else if (fast) {
     // a row of <= CH * NT * 4 floats (GPT-2's) is loaded ONCE and every pass
     // runs from registers (the tail past V masked to -inf at load time, so
     // no per-element bounds checks); longer rows (Llama-3's) re-read via L2
@@ -186,27 +303,8 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     } else {
       for_row(x, V, [&](float val, int) { mx = fmaxf(mx, val); });
     }
-    mx = fmaxf(mx, wave_xchg<1>(mx));
-    mx = fmaxf(mx, wave_xchg<2>(mx));
-    mx = fmaxf(mx, wave_xchg<4>(mx));
-    mx = fmaxf(mx, wave_xchg<8>(mx));
-    if ((tid & 15) == 0) cval[tid >> 4] = mx;
     if (tid == 0) s_cnt = 0;
-    __syncthreads();
-    if (tid < 64) {  // rank of segment `tid` among the 64 maxima (ties by segment)
-      const float sv = cval[tid];
-      int rank = 0;
-#pragma unroll
-      for (int j4 = 0; j4 < 16; ++j4) {
-        const f32x4 o = reinterpret_cast<const f32x4*>(cval)[j4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) rank += (o[e] > sv || (o[e] == sv && 4 * j4 + e < tid)) ? 1 : 0;
-      }
-      if (rank == k - 1) redv[0] = sv;
-    }
-    __syncthreads();
-    const float tau = redv[0];
-    const int lane = lane_id();
+    const float tau = kth_group_max(mx, k, cval, redv);
     // compaction without per-element atomics: per-thread candidate count (and
     // bit mask of register positions), wave scan, one LDS atomic per wave
     int cnt = 0;
@@ -224,15 +322,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     } else {
       for_row(x, V, [&](float val, int) { cnt += val >= tau ? 1 : 0; });
     }
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int o = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += o;
-    }
-    unsigned base = 0;
-    if (lane == 63) base = atomicAdd(&s_cnt, (unsigned)incl);
-    unsigned slot = __shfl(base, 63, 64) + (unsigned)(incl - cnt);
+    unsigned slot = claim_slots(cnt, &s_cnt);
     if (one) {
       while (msk) {  // ~0-2 trips per thread; the value comes back from L2
         const int e = __builtin_ctzll(msk);
@@ -463,10 +553,10 @@ using namespace lsd;
 extern "C" hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                                  const int* topk, const int* greedy, const long long* seeds,
                                  long long* step, int* out, int advance, const int* active,
-                                 int* pos, hipStream_t st) {
+                                 int* pos, const float* segmax, long ldseg, hipStream_t st) {
   if (B == 0) return hipSuccess;
   if (ld % 4 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(NT), 0, st, logits, ld, V, temp, topk, greedy,
-                     seeds, step, out, advance, active, pos);
+                     seeds, step, out, advance, active, pos, segmax, ldseg);
   return hipGetLastError();
 }

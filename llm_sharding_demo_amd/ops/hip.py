@@ -210,6 +210,8 @@ class HipBackend(Backend):
     # (p50 8.72 ms: 96 KiB of LDS per workgroup), so 3 slots.
     RING8 = int(os.environ.get("LSD_RING8", "2"))
     RING8_FLAGS = int(os.environ.get("LSD_RING8_FLAGS", "0"))  # A/B bits (gemm.hip)
+    # lm_head epilogue writes 8-logit segment maxima for the sampler (sample.hip)
+    SEGMAX = int(os.environ.get("LSD_SEGMAX", "1"))
     # K splits of the non-residual decode GEMMs on the 8-wave ring (QKV, MLP-up,
     # 129-256 rows) with the in-kernel last-arriver combine: aim at this many
     # workgroups (0 = off: one workgroup per 128x64 tile)
@@ -545,20 +547,31 @@ class HipBackend(Backend):
         # of once per 64 -- measured 41.8 vs 64.2 us at M = 128 (GPT-2 XL),
         # 222.7 vs 300.3 us for Llama-3 8B (tools/microbench.py lmhead)
         if w.shape[0] >= 16384 and w.shape[1] % 64 == 0:
-            return self.C.linear_f32(xn, w, True, 1, self.counters)
-        tiled, splits = self._gemm_kw(xn.shape[0], w.shape[0], w.shape[1])
-        return self.C.linear_f32(xn, w, tiled, splits, self.counters)
+            tiled, splits = True, 1
+        else:
+            tiled, splits = self._gemm_kw(xn.shape[0], w.shape[0], w.shape[1])
+        if not (self.SEGMAX and tiled and w.shape[0] % 8 == 0):
+            return self.C.linear_f32(xn, w, tiled, splits, self.counters)
+        # the epilogue also writes each 8-logit segment's maximum; the sampler
+        # derives its top-k threshold from them and reads only the segments
+        # that reach it (attached to the logits: a slice drops it, and the
+        # sampler then scans the full rows)
+        seg = torch.empty(xn.shape[0], w.shape[0] // 8, dtype=torch.float32, device=xn.device)
+        out = self.C.linear_f32(xn, w, tiled, splits, self.counters, seg)
+        out._lsd_segmax = seg
+        return out
 
     def sample(self, logits, samp, vocab: int):
         return self.C.sample(logits, vocab, samp.temperature, samp.top_k, samp.greedy,
-                             samp.seeds, samp.step)
+                             samp.seeds, samp.step, getattr(logits, "_lsd_segmax", None))
 
     def sample_into(self, logits, samp, vocab: int, out, meta=None) -> None:
         # one kernel: draw into `out`, advance the per-row sampler counters
         # and (meta given) the decode batch's positions
         self.C.sample_into(logits, vocab, samp.temperature, samp.top_k, samp.greedy,
                            samp.seeds, samp.step, out, getattr(samp, "active", None),
-                           meta.token_pos if meta is not None else None)
+                           meta.token_pos if meta is not None else None,
+                           getattr(logits, "_lsd_segmax", None))
 
     def gather_rows(self, x, idx):
         return x.index_select(0, idx.long())

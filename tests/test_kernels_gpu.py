@@ -618,6 +618,27 @@ def test_attention_prefill_large_logits_stable(C):
     close(o.reshape(-1, nh, hd), o_ref, 3e-2)
 
 
+@pytest.mark.parametrize("M,N,K,kind,splits", [(1, 1040, 128, 1, 1), (64, 1040, 640, 1, 1),
+                                                (200, 1040, 640, 1, 1), (256, 50304, 1600, 1, 1),
+                                                (512, 4096, 256, 1, 1), (256, 4800, 1600, 2, 2),
+                                                (100, 352, 640, 3, 3)])
+def test_linear_f32_segmax(C, CNT, M, N, K, kind, splits):
+    """lm_head epilogue: fp32 logits plus the max of every 8-column segment,
+    bit-equal to the maximum of the stored logits, on every tiled kernel the
+    grid size routes to (ring, 8-wave ring, 256^2, 256-row split-K)."""
+    a, w = bf(M, K, seed=90), bf(N, K, scale=0.05, seed=91)
+    seg = torch.full((M, N // 8), float("nan"), device=DEV)
+    out = C.linear_f32(a, w, kind, splits, CNT, seg)
+    close(out, ref.linear(a, w), 2e-3, 1e-3)
+    assert torch.equal(seg, out.view(M, N // 8, 8).amax(-1))
+
+
+def _segmax(logits):
+    """What linear_f32 writes beside these logits (padding columns included)."""
+    B, Vp = logits.shape
+    return logits.view(B, Vp // 8, 8).amax(-1).contiguous()
+
+
 def test_sampler(C):
     from llm_sharding_demo_amd.runtime.batch import counter_uniform
 
@@ -653,11 +674,14 @@ def test_sampler(C):
         assert int(out[r]) in set(torch.topk(logits[r, :V], k).indices.tolist())
 
 
+@pytest.mark.parametrize("seg", [False, True])
 @pytest.mark.parametrize("case", ["random", "ties", "flat", "quantized", "llama_vocab"])
-def test_sampler_fast_path_and_ties(C, case):
-    """top-k <= 64 takes the threshold/filter path; flat logits (more
-    candidates than fit) fall back to the radix path; ties are broken by the
-    lowest index in both -- bit-equal to the host reference either way."""
+def test_sampler_fast_path_and_ties(C, case, seg):
+    """top-k <= 64 takes the threshold/filter path (seg: its threshold from
+    lm_head's 8-logit segment maxima, reading only the segments that reach
+    it; the partial last segment's maximum includes the padding); flat logits
+    (more candidates than fit) fall back to the radix path; ties are broken
+    by the lowest index in both -- bit-equal to the host reference either way."""
     from llm_sharding_demo_amd.runtime.batch import counter_uniform
 
     B, V, Vp = (12, 128256, 128256) if case == "llama_vocab" else (12, 50257, 50304)
@@ -675,24 +699,26 @@ def test_sampler_fast_path_and_ties(C, case):
     greedy = torch.tensor([0] * 11 + [1], dtype=torch.int32, device=DEV)
     seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 104729 + 11
     step = torch.arange(B, dtype=torch.int64, device=DEV)
-    out = C.sample(logits, V, temp, topk, greedy, seeds, step)
+    sm = _segmax(logits) if seg else None
+    out = C.sample(logits, V, temp, topk, greedy, seeds, step, sm)
     exp = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), greedy.cpu(),
                      counter_uniform(seeds.cpu(), step.cpu()), V)
     assert out.cpu().tolist() == exp.tolist()
     # decode-step form: same draw written into a slice, counters advanced in-kernel
     buf = torch.full((B + 3,), -1, dtype=torch.int32, device=DEV)
     st2 = step.clone()
-    C.sample_into(logits, V, temp, topk, greedy, seeds, st2, buf[:B], None)
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st2, buf[:B], None, None, sm)
     assert buf[:B].cpu().tolist() == exp.tolist() and buf[B:].cpu().tolist() == [-1] * 3
     assert torch.equal(st2, step + 1)
     act = (torch.arange(B, device=DEV) % 3 != 0).int()  # pad rows (0) keep their counter
     st3 = step.clone()
-    C.sample_into(logits, V, temp, topk, greedy, seeds, st3, buf[:B], act)
+    C.sample_into(logits, V, temp, topk, greedy, seeds, st3, buf[:B], act, None, sm)
     assert buf[:B].cpu().tolist() == exp.tolist() and torch.equal(st3, step + act)
 
 
-@pytest.mark.parametrize("V,Vp", [(1000, 1024), (1000, 1000), (3000, 3008)])
-def test_sampler_small_vocab(C, V, Vp):
+@pytest.mark.parametrize("seg", [False, True])
+@pytest.mark.parametrize("V,Vp", [(1000, 1024), (1000, 1000), (3000, 3008), (2997, 3008)])
+def test_sampler_small_vocab(C, V, Vp, seg):
     """V < 4096 (the test presets): fewer than k of the 64 segments hold real
     logits, so the fast path's threshold is -inf -- padding past V must never
     become a candidate (its index lies past the row).  The rows sit
@@ -710,7 +736,7 @@ def test_sampler_small_vocab(C, V, Vp):
     greedy = torch.zeros(B, dtype=torch.int32, device=DEV)
     seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 31 + 1
     step = torch.arange(B, dtype=torch.int64, device=DEV)
-    out = C.sample(logits, V, temp, topk, greedy, seeds, step)
+    out = C.sample(logits, V, temp, topk, greedy, seeds, step, _segmax(logits) if seg else None)
     exp = ref.sample(logits.cpu(), temp.cpu(), topk.cpu(), greedy.cpu(),
                      counter_uniform(seeds.cpu(), step.cpu()), V)
     assert out.cpu().tolist() == exp.tolist()

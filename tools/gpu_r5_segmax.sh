@@ -1,0 +1,22 @@
+#!/bin/bash
+# round 5: lm_head segment maxima + sampler -- kernel tests, engine tests,
+# lm_head+sample microbench, headline bench A/B (interleaved)
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+L=gpurun_out/r5_segmax.log
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
+  -p no:cacheprovider -k "sampler or segmax" > gpurun_out/r5_segmax_tests.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py tests/test_numerics_gpu.py -m gpu -x -q --timeout 300 \
+  --timeout-method thread -p no:cacheprovider >> gpurun_out/r5_segmax_tests.log 2>&1 || exit $?
+echo "== microbench lmsample" > $L
+timeout -k 10 300 python -u tools/microbench.py lmsample >> $L 2>&1 || exit $?
+for i in 1 2; do
+  for sg in 1 0; do
+    echo "== bench LSD_SEGMAX=$sg (round $i)" >> $L
+    LSD_SEGMAX=$sg timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 >> $L 2>&1 || exit $?
+  done
+done
+for sg in 1 0; do
+  echo "== bench gpt2 small LSD_SEGMAX=$sg" >> $L
+  LSD_SEGMAX=$sg timeout -k 10 300 python -u bench.py --model gpt2 --steps 3 --warmup 1 >> $L 2>&1 || exit $?
+done

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import json
 import math
+import statistics
 import os
 import sys
 
@@ -446,6 +447,45 @@ def bench_lmhead_kinds(M=256, N=50304, K=1600):
     report(f"lmhead_hipblaslt M={M} N={N} K={K}", timeit(ref), N * K * 2)
 
 
+def bench_lmhead_sample(M=256, V=50257, K=1600):
+    """Decode head: lm_head (fp32 logits) + the sampler (T 0.6, top-k 40), with
+    and without the epilogue's 8-logit segment maxima; rotating weights,
+    interleaved rounds; asserts equal draws."""
+    Vp = (V + 63) // 64 * 64
+    ws = rotating(lambda: torch.randn(Vp, K, device=DEV).mul_(0.05).bfloat16(), Vp * K * 2)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    t = torch.full((M,), 0.6, device=DEV)
+    k = torch.full((M,), 40, dtype=torch.int32, device=DEV)
+    g = torch.zeros(M, dtype=torch.int32, device=DEV)
+    sd = torch.arange(M, dtype=torch.int64, device=DEV)
+    st = torch.zeros(M, dtype=torch.int64, device=DEV)
+    it = [0]
+    outs = {}
+
+    def run(seg, sample=True):
+        def f():
+            w = ws[it[0] % len(ws)]
+            it[0] += 1
+            sm = torch.empty(M, Vp // 8, device=DEV) if seg else None
+            lg = C.linear_f32(a, w, True, 1, None, sm)
+            if sample:
+                outs[seg] = C.sample(lg, V, t, k, g, sd, st, sm)
+        return f
+    for seg in (False, True):
+        it[0] = 0
+        run(seg)()
+    torch.cuda.synchronize()
+    assert torch.equal(outs[False], outs[True])
+    res = {c: [] for c in ("gemm", "gemm+seg", "full", "seg")}
+    for _ in range(5):
+        res["gemm"].append(timeit(run(False, False)))
+        res["gemm+seg"].append(timeit(run(True, False)))
+        res["full"].append(timeit(run(False)))
+        res["seg"].append(timeit(run(True)))
+    for c, v in res.items():
+        report(f"lmhead_sample_{c} M={M} V={V} K={K}", statistics.median(v), Vp * K * 2)
+
+
 def bench_llama_decode_kinds(M=256):
     """Llama-3 8B decode GEMMs at M rows under each tiled-kernel choice:
     128x128 double buffer, LDS ring 128x64 / 128x128, phase-pipelined 256x256."""
@@ -658,6 +698,11 @@ def main():
     if "p8prof" in which:  # LSD_P8_PROF build: loop cycles split into vmcnt waits and the two barriers
         stamps_p8(act=0)
         stamps_p8(M=4096, N=4096, K=4096, act=0)
+    if "lmsample" in which:  # lm_head + sampler, segment maxima on / off
+        bench_lmhead_sample(256, 50257, 1600)
+        bench_lmhead_sample(256, 50257, 768)
+        bench_lmhead_sample(128, 50257, 1600)
+        bench_lmhead_sample(256, 128256, 4096)
     if "lmk" in which:
         for M in (256, 512):
             bench_lmhead_kinds(M)
