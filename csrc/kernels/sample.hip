@@ -16,9 +16,10 @@
 //           passes over bits [31:20], [19:8], [7:0] (4096/4096/256 bins; the
 //           exponent-heavy top bits are spread over 4096 bins so LDS atomics
 //           do not pile onto a few hot bins), each bin search a block-parallel
-//           suffix scan.  The k winners are sorted by (value desc, index asc)
-//           with a bitonic network in LDS (deterministic regardless of atomic
-//           arrival order), softmax over value/T, inverse-CDF draw with
+//           suffix scan.  The winners / candidates are ordered by (value
+//           desc, index asc) -- rank selection for k <= 128, a bitonic
+//           network in LDS above (deterministic regardless of atomic arrival
+//           order) -- then softmax over value/T, inverse-CDF draw with
 //           u = splitmix64(seed * FNV + step) -- the same counter-based
 //           generator as runtime/batch.py:counter_uniform, so a seeded
 //           request reproduces across batch layouts and stage counts.
@@ -162,8 +163,8 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
                                                     int* __restrict__ pos,
                                                     const float* __restrict__ segmax, long ldseg) {
   __shared__ unsigned hist[4096];
-  __shared__ float cval[SMAX];
-  __shared__ int cidx[SMAX];
+  __shared__ __attribute__((aligned(16))) float cval[SMAX];
+  __shared__ __attribute__((aligned(16))) int cidx[SMAX];
   __shared__ unsigned tmp[32];
   __shared__ float redv[16];
   __shared__ int redi[16];
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
   // segment maxima are k distinct elements >= tau), so {x >= tau} holds the
   // top k.  One pass for the maxima + one filter pass (the row stays in L2),
   // ~100 candidates on real or random logits; the exact (value desc, index
-  // asc) order comes from the bitonic sort below, so the result equals the
+  // asc) order comes from the rank selection below, so the result equals the
   // radix path's.  More than SMAX candidates (flat logits) -> radix path.
   bool fast = k <= 64;
   const int S = (V + 7) >> 3;  // 8-logit segments holding real logits (the last may be partial)
@@ -424,45 +425,48 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     }
   }
   }  // radix path
-  // ---- <= 128 entries (fast-path candidates, or k <= 128 radix winners): wave 0 sorts them in
-  // registers (2 per lane, element e = 2 * lane + r, cross-lane steps by
-  // shuffles) and draws without another block barrier.
-  if (nsel <= 128) {
+  // ---- k <= 128 (every fast-path row; radix rows with k <= 128): rank
+  // selection -- thread t counts the entries ahead of entry t in (value desc,
+  // index asc) order (LDS broadcast reads, 4 per instruction) and, ranked < k,
+  // writes it there: independent work and one barrier for any nsel <= SMAX,
+  // instead of a sorting network (a wave network of 28 dependent shuffle
+  // stages for <= 128 entries, a barrier per stage in LDS beyond that, which
+  // the rows with more than 128 candidates hit).  The draw: wave 0, 2 sorted
+  // entries per lane (element e = 2 * lane + r).  Sampler 256 rows x GPT-2
+  // vocab, top-k 40: 21.7 -> 20.8 us (16.5 with the segment maxima),
+  // profiles/r5_sampler_ab.log.  Rank counting is O(nsel) per thread: rows
+  // with more than 256 candidates (top-k 64 takes the smallest of the 64
+  // group maxima as its threshold: ~500) keep the LDS network (top-k 64:
+  // 65 us ranked vs 32 us sorted, profiles/r5_sampler_final.log).
+  if (k <= 128 && nsel <= 256) {
+    float* sv = reinterpret_cast<float*>(hist);
+    int* si = reinterpret_cast<int*>(hist + SMAX);
+    if (tid < nsel) {
+      const float cv = cval[tid];
+      const int ci = cidx[tid];
+      int rk = 0;
+      for (int j4 = 0; j4 < nsel; j4 += 4) {
+        const f32x4 vv = *reinterpret_cast<const f32x4*>(cval + j4);
+        const int4 ii = *reinterpret_cast<const int4*>(cidx + j4);
+        const float vj[4] = {vv[0], vv[1], vv[2], vv[3]};
+        const int ij[4] = {ii.x, ii.y, ii.z, ii.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          rk += (j4 + e < nsel && (vj[e] > cv || (vj[e] == cv && ij[e] < ci))) ? 1 : 0;
+      }
+      if (rk < k) { sv[rk] = cv; si[rk] = ci; }
+    }
+    __syncthreads();
     if (tid >= 64) return;
-    const int e0 = 2 * tid;
     float v[2];
     int ix[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      const bool ok = e0 + r < nsel;
-      v[r] = ok ? cval[e0 + r] : -INFINITY;
-      ix[r] = ok ? cidx[e0 + r] : 0x7fffffff;
+      const bool ok = 2 * tid + r < k;
+      v[r] = ok ? sv[2 * tid + r] : -INFINITY;
+      ix[r] = ok ? si[2 * tid + r] : 0x7fffffff;
     }
-#pragma unroll
-    for (int size = 2; size <= 128; size <<= 1) {
-#pragma unroll
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        if (stride == 1) {
-          const bool up = (e0 & size) == 0;
-          const bool first = v[0] > v[1] || (v[0] == v[1] && ix[0] < ix[1]);
-          if (up != first) {
-            const float tv = v[0]; v[0] = v[1]; v[1] = tv;
-            const int ti = ix[0]; ix[0] = ix[1]; ix[1] = ti;
-          }
-        } else {
-          const int pl = stride >> 1;  // partner lane = lane ^ pl, same r
-          const bool lower = (tid & pl) == 0;
-#pragma unroll
-          for (int r = 0; r < 2; ++r) {
-            const bool up = ((e0 + r) & size) == 0;
-            const float pv = shfl_xor(v[r], pl);
-            const int pi = shfl_xor(ix[r], pl);
-            const bool own_first = v[r] > pv || (v[r] == pv && ix[r] < pi);
-            if (lower ? (own_first != up) : (own_first == up)) { v[r] = pv; ix[r] = pi; }
-          }
-        }
-      }
-    }
+    const int e0 = 2 * tid;
     const float x0 = __shfl(v[0], 0, 64) / T;
     const float u = counter_uniform(seed_r, step_r);
     const float p0 = e0 < k ? __expf(v[0] / T - x0) : 0.f;
@@ -487,7 +491,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
     }
     return;
   }
-  // ---- bitonic sort of the winners / candidates: (value desc, index asc); pad to pow2
+  // ---- k > 128 or nsel > 256: bitonic sort of the winners / candidates: (value desc, index asc); pad to pow2
   int n2 = 1;
   while (n2 < nsel) n2 <<= 1;
   for (int i = nsel + tid; i < n2; i += NT) { cval[i] = -INFINITY; cidx[i] = 0x7fffffff; }
@@ -546,6 +550,7 @@ __global__ __launch_bounds__(NT) void sample_kernel(const float* __restrict__ lo
 }  // namespace lsd
 
 using namespace lsd;
+
 
 // advance != 0: also step[row] += active[row] (1 when active is null) after
 // the draw -- the decode step's sampler-counter advance (pad rows stay put),
