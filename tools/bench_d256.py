@@ -29,6 +29,16 @@ SHAPES = {  # name: (N, K, kind)  kind: act code, or "resid"
     "l8_down": (4096, 14336, "resid"),
     "s_qkv": (2304, 768, 0), "s_fc": (3072, 768, 1), "s_proj": (768, 768, "resid"),
     "s_proj2": (768, 3072, "resid"),
+    # vocabulary projections (fp32 logits, the decode head)
+    "xl_lm": (50304, 1600, "f32"), "s_lm": (50304, 768, "f32"), "l8_lm": (128256, 4096, "f32"),
+}
+
+# launch-routing knobs for the f32 (lm_head) variants, read at launch (capture) time
+KNOBS = {
+    "big": lambda on: C.gemm_set_big_kind(2 if on else 4),          # gemm_big_kernel instead of p8
+    "nop8": lambda on: C.gemm_set_big_min((1 << 30) if on else 160),  # no 256x256 kernel: 128-row tiles
+    "r8": lambda on: (C.gemm_set_big_min((1 << 30) if on else 160),    # 8-wave 128x64 ring
+                      C.gemm_set_tiled3_max((1 << 30) if on else HipBackend.TILED3_MAX)),
 }
 
 
@@ -84,7 +94,8 @@ def main():
             x0 = torch.randn(M, N, device=DEV)
             bias = torch.randn(N, device=DEV).mul_(0.1).bfloat16()
             resid = kind == "resid"
-            act = 0 if resid else kind
+            f32 = kind == "f32"
+            act = 0 if (resid or f32) else kind
 
             def make(bn, S, r8=0):
                 it = [0]
@@ -93,10 +104,17 @@ def main():
                 kind = 3 if bn == 128 else 2
 
                 def run():
-                    C.gemm_set_ring8(r8 & 15)  # read at launch (capture) time
-                    C.gemm_set_ring8_flags((r8 >> 4) & 15)
+                    C.gemm_set_ring8(r8 & 15 if not isinstance(r8, str) else HipBackend.RING8)  # read at launch
+                    C.gemm_set_ring8_flags((r8 >> 4) & 15 if not isinstance(r8, str) else 0)
                     w = ws[it[0] % nw]
                     it[0] += 1
+                    if f32:
+                        if isinstance(r8, str):
+                            KNOBS[r8](True)
+                        y = C.linear_f32(a, w, True if bn == 0 else kind, 1 if bn == 0 else S, cnt)
+                        if isinstance(r8, str):
+                            KNOBS[r8](False)
+                        return y
                     if resid:
                         if bn == 0:
                             s2 = be._resid_splits(M, N, K)
@@ -117,6 +135,10 @@ def main():
 
             cases = [("ring", 0, 1, int(os.environ.get("D256_BASE_R8", "0")))]
             for v in variants:
+                if v.startswith("knob:"):  # f32 shapes: a launch-routing knob (KNOBS)
+                    if f32:
+                        cases.append((v[5:], 0, 1, v[5:]))
+                    continue
                 if v.startswith("r8s:"):  # 8-wave ring, S K splits + in-kernel combine
                     C.gemm_set_ring8(2)
                     if not resid and C.gemm_ring8_tiles(M, N, K, int(v[4:])):
