@@ -657,12 +657,14 @@ void sample_into(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Ten
 void lsd_register_comm(pybind11::module& m);  // csrc/comm.cpp
 void lsd_register_exec(pybind11::module& m);  // csrc/stage_exec.cpp
 void lsd_register_loopback(pybind11::module& m);  // csrc/loop_fabric.cpp
+void lsd_register_blaslt(pybind11::module& m);    // csrc/blaslt.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "CDNA4 (gfx950) kernels for llm_sharding_demo_amd";
   lsd_register_comm(m);
   lsd_register_exec(m);
   lsd_register_loopback(m);
+  lsd_register_blaslt(m);
   m.def("linear", &linear);
   m.def("linear_f32", &linear_f32, py::arg("a"), py::arg("w"), py::arg("tiled"), py::arg("splits"),
         py::arg("counters"), py::arg("segmax") = py::none());

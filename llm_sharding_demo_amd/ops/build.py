@@ -29,8 +29,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 KERNELS = ["gemm.hip", "gemv.hip", "norm.hip", "attention.hip", "sample.hip", "loopback.hip"]
 # host code of the extension: kernel bindings, native RCCL communicator, native stage
-# executor, device loopback channels (single-GPU rehearsal of the RCCL edges)
-HOST_SOURCES = ["bindings.cpp", "comm.cpp", "stage_exec.cpp", "loop_fabric.cpp"]
+# executor, device loopback channels (single-GPU rehearsal of the RCCL edges),
+# hipBLASLt prefill projections
+HOST_SOURCES = ["bindings.cpp", "comm.cpp", "stage_exec.cpp", "loop_fabric.cpp", "blaslt.cpp"]
 EXT_NAME = "_C"
 
 
@@ -112,7 +113,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
         tmp = so + ".tmp"
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs +
              ["-o", tmp, f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
-              "-ltorch_python", "-ltorch_hip", "-ldl", f"-Wl,-rpath,{torch_lib}"], verbose)
+              "-ltorch_python", "-ltorch_hip", "-lhipblaslt", "-ldl", f"-Wl,-rpath,{torch_lib}"], verbose)
         os.replace(tmp, so)
     return so
 

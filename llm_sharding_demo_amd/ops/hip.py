@@ -132,6 +132,10 @@ class HipBackend(Backend):
     # prefill 222.6 / 225.1 vs 224.5 / 225.8 ms on the headline, within noise
     # (profiles/r5_prefill_slab_ab.log) -- opt-in (LSD_PREFILL_SLAB=1)
     PREFILL_SLAB = os.environ.get("LSD_PREFILL_SLAB", "0") == "1"
+    # prefill MLP-up (bias + GELU) and residual projections (x += a w^T + b) with
+    # at least this many rows go to hipBLASLt, which fuses those epilogues
+    # itself (csrc/blaslt.cpp); 0 = always the hand-written kernels
+    BLASLT_MIN_M = int(os.environ.get("LSD_BLASLT_MIN_M", "4096"))
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
     # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:
@@ -508,8 +512,15 @@ class HipBackend(Backend):
             return self.C.gemv(x, w, b, code, nc, gw, gb, eps, None, None, None, None, None,
                                0, 0, 0, None)
         a = self.materialize(a)
+        if code in (0, 1) and self._blaslt(a.shape[0]) and a.is_contiguous():
+            y = self.C.blaslt_linear(a, w, b, code)
+            if y is not None:
+                return y
         tiled, splits = self._gemm_kw(a.shape[0], w.shape[0], w.shape[1], 2 if code == 2 else 1)
         return self.C.linear(a, w, b, code, tiled, splits, self.counters)
+
+    def _blaslt(self, M: int) -> bool:
+        return bool(self.BLASLT_MIN_M) and M >= self.BLASLT_MIN_M and not getattr(self, "decode", True)
 
     def linear_residual(self, a, w, b, r: Residual) -> None:
         M, K = a.shape
@@ -517,6 +528,8 @@ class HipBackend(Backend):
         if self._gemv_in(a, K, EPI_RESID) is not None:  # adds straight into r.x
             self.C.gemv(a, w, b, EPI_RESID, 0, None, None, 0.0, r.x, None, None, None, None,
                         0, 0, 0, None)
+            return
+        if self._blaslt(M) and a.is_contiguous() and self.C.blaslt_residual(a, w, b, r.x):
             return
         splits = self._resid_splits(M, N, K)
         tiled = self._tiled(M, N)

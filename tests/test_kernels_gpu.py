@@ -633,6 +633,26 @@ def test_linear_f32_segmax(C, CNT, M, N, K, kind, splits):
     assert torch.equal(seg, out.view(M, N // 8, 8).amax(-1))
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 1600, 1600), (4100, 6400, 1600), (8192, 768, 3072)])
+def test_blaslt_prefill_projections(C, M, N, K):
+    """hipBLASLt prefill projections (csrc/blaslt.cpp): bf16 out with bias and
+    bias + GELU epilogues, and the fp32 residual accumulate (beta = 1, C = D =
+    x) -- against the fp32 reference; the library's GELU against GPT-2's
+    tanh-approximated gelu_new at bf16 resolution."""
+    a, w, bias = bf(M, K, seed=95), bf(N, K, scale=0.05, seed=96), bf(N, scale=0.1, seed=97)
+    y_ref = ref.linear(a, w, bias)
+    y = C.blaslt_linear(a, w, bias, 0)
+    assert y is not None, "hipBLASLt has no algorithm for the prefill shape"
+    close(y, y_ref, 3e-2)
+    close(C.blaslt_linear(a, w, bias, 1), ref.gelu_new(y_ref), 3e-2)
+    close(C.blaslt_linear(a, w, None, 1), ref.gelu_new(ref.linear(a, w)), 3e-2)
+    for b in (bias, None):
+        x = torch.randn(M, N, device=DEV)
+        x_ref = x + ref.linear(a, w, b)
+        assert C.blaslt_residual(a, w, b, x)
+        close(x, x_ref, 2e-3, 1e-3)
+
+
 def _segmax(logits):
     """What linear_f32 writes beside these logits (padding columns included)."""
     B, Vp = logits.shape

@@ -49,7 +49,37 @@ def case(label, M, N, K, act=0, resid=False, kinds=(1,)):
     print(json.dumps(row), flush=True)
 
 
+def blaslt_case(label, M, N, K, resid):
+    """Engine routing A/B: the hand-written 256x256 kernel with its fused epilogue
+    vs hipBLASLt with the library's (csrc/blaslt.cpp), bias included."""
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    w = torch.randn(N, K, device=DEV).mul_(0.05).bfloat16()
+    b = torch.randn(N, device=DEV).mul_(0.1).bfloat16()
+    x = torch.randn(M, N, device=DEV)
+    fl = 2.0 * M * N * K
+    if resid:
+        ours = lambda: C.linear_residual(a, w, b, x, 1, True, None, False)  # noqa: E731
+        lt = lambda: C.blaslt_residual(a, w, b, x)  # noqa: E731
+    else:
+        ours = lambda: C.linear(a, w, b, 1, True, 1, None)  # noqa: E731
+        lt = lambda: C.blaslt_linear(a, w, b, 1)  # noqa: E731
+    row = {"case": label, "M": M, "N": N, "K": K}
+    for name, fn in (("p8", ours), ("blaslt", lt)):
+        us = min(timeit(fn, iters=10) for _ in range(3))
+        row[f"{name}_us"] = round(us, 1)
+        row[f"{name}_TF"] = round(fl / us / 1e6, 1)
+    print(json.dumps(row), flush=True)
+
+
 def main():
+    if sys.argv[1:] == ["blaslt"]:
+        for M in (32768, 65536):
+            blaslt_case("xl_fc_gelu", M, 6400, 1600, False)
+            blaslt_case("xl_proj_resid", M, 1600, 1600, True)
+            blaslt_case("xl_proj2_resid", M, 1600, 6400, True)
+        blaslt_case("l8_o_resid", 32768, 4096, 4096, True)
+        blaslt_case("l8_down_resid", 32768, 4096, 14336, True)
+        return
     kinds = tuple(int(v) for v in sys.argv[1:]) or (1,)
     case("sq4096", 4096, 4096, 4096, kinds=kinds)
     case("sq8192", 8192, 8192, 8192, kinds=kinds)
