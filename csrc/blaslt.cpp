@@ -15,8 +15,8 @@
 //
 // One handle, workspace and heuristic cache per device; the first call of a
 // (M, N, K, epilogue) asks the heuristic and keeps its first algorithm.
-// blaslt_available() is false when the library finds no algorithm (the
-// caller then keeps the hand-written kernel).
+// The bindings report "no algorithm" (None / false, nothing issued) and the
+// caller then keeps the hand-written kernel.
 #include <torch/extension.h>
 
 #include <ATen/hip/HIPContext.h>
@@ -74,7 +74,9 @@ Plan& plan(DeviceState& s, long M, long N, long K, hipblasLtEpilogue_t epi, bool
   lt_check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)), "transa");
   lt_check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)), "transb");
   lt_check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)), "epilogue");
-  const hipDataType bt = HIP_R_16BF;
+  // the bias type must be D's or the scale type's: bf16 with a bf16 D, fp32
+  // (converted per call, N floats) with the fp32 residual
+  const hipDataType bt = f32out ? HIP_R_32F : HIP_R_16BF;
   lt_check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)), "bias type");
   lt_check(hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, N, K), "layout A");
   lt_check(hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, K, M, K), "layout B");
@@ -154,7 +156,10 @@ void lsd_register_blaslt(pybind11::module& m) {
     const long M = a.size(0), N = w.size(0), K = a.size(1);
     TORCH_CHECK(x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 2 && x.size(0) == M &&
                 x.size(1) == N, "blaslt_residual: x must be contiguous fp32 [M, N]");
-    const void* b = bias_ptr(bias, N);
+    bias_ptr(bias, N);  // checks
+    torch::Tensor b32;
+    if (bias.has_value()) b32 = bias->to(torch::kFloat32);
+    const void* b = bias.has_value() ? b32.data_ptr() : nullptr;
     std::lock_guard<std::mutex> lk(g_mu);
     auto& s = state(a);
     auto& p = plan(s, M, N, K, b ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT, true);

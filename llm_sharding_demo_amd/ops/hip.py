@@ -132,10 +132,16 @@ class HipBackend(Backend):
     # prefill 222.6 / 225.1 vs 224.5 / 225.8 ms on the headline, within noise
     # (profiles/r5_prefill_slab_ab.log) -- opt-in (LSD_PREFILL_SLAB=1)
     PREFILL_SLAB = os.environ.get("LSD_PREFILL_SLAB", "0") == "1"
-    # prefill MLP-up (bias + GELU) and residual projections (x += a w^T + b) with
-    # at least this many rows go to hipBLASLt, which fuses those epilogues
-    # itself (csrc/blaslt.cpp); 0 = always the hand-written kernels
+    # prefill GEMMs hipBLASLt runs with its own fused epilogues (csrc/blaslt.cpp),
+    # where it measured faster than the hand-written 256x256 kernel
+    # (profiles/r5_blaslt.log): residual projections (x += a w^T + b, fp32 x)
+    # with K >= BLASLT_RESID_MIN_K (GPT-2 XL proj2 +5 %, Llama-3 8B o / down
+    # +6 %; K 1600 loses 12 % at 32 K rows) and MLP-up bias + GELU from
+    # BLASLT_GELU_MIN_M rows (+11 % at 64 K rows, a tie at 32 K).  Only at or
+    # above BLASLT_MIN_M rows (0 = never).
     BLASLT_MIN_M = int(os.environ.get("LSD_BLASLT_MIN_M", "4096"))
+    BLASLT_RESID_MIN_K = int(os.environ.get("LSD_BLASLT_RESID_MIN_K", "4096"))
+    BLASLT_GELU_MIN_M = int(os.environ.get("LSD_BLASLT_GELU_MIN_M", "65536"))
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
     # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:
@@ -512,7 +518,8 @@ class HipBackend(Backend):
             return self.C.gemv(x, w, b, code, nc, gw, gb, eps, None, None, None, None, None,
                                0, 0, 0, None)
         a = self.materialize(a)
-        if code in (0, 1) and self._blaslt(a.shape[0]) and a.is_contiguous():
+        if code == 1 and self._blaslt(a.shape[0]) and a.shape[0] >= self.BLASLT_GELU_MIN_M \
+                and a.is_contiguous():
             y = self.C.blaslt_linear(a, w, b, code)
             if y is not None:
                 return y
@@ -529,7 +536,8 @@ class HipBackend(Backend):
             self.C.gemv(a, w, b, EPI_RESID, 0, None, None, 0.0, r.x, None, None, None, None,
                         0, 0, 0, None)
             return
-        if self._blaslt(M) and a.is_contiguous() and self.C.blaslt_residual(a, w, b, r.x):
+        if self._blaslt(M) and K >= self.BLASLT_RESID_MIN_K and a.is_contiguous() \
+                and self.C.blaslt_residual(a, w, b, r.x):
             return
         splits = self._resid_splits(M, N, K)
         tiled = self._tiled(M, N)
