@@ -208,6 +208,10 @@ class GroupState(racecheck.Shared):
         # loopback graph I/O: key -> (native I/O-list handle, [(chan, dir, bytes)])
         self.graph_io: Dict[tuple, tuple] = {}
         self.seen: set = set()
+        # prefill chunks of a recurring shape: (qlens, variant, input buffer)
+        # -> (graph, packed index buffer, static meta, output); see _prefill_graph
+        self.pf_graphs: Dict[tuple, tuple] = {}
+        self.pf_seen: set = set()
         self._metas: Dict[tuple, BatchMeta] = {}
         self.rows_n = 0
 
@@ -243,6 +247,8 @@ class GroupState(racecheck.Shared):
         self.graph_io.clear()
         self.graphs.clear()
         self.seen.clear()
+        self.pf_graphs.clear()
+        self.pf_seen.clear()
 
     def meta(self, b: int, ctxb: int) -> BatchMeta:
         key = (b, ctxb)
@@ -345,6 +351,7 @@ class StageWorker(racecheck.Shared):
         self.send_pending: Dict[int, List[SendHandle]] = {}
         self.recv: Dict[tuple, List[Handle]] = {}
         self.captures = 0          # hipGraph captures so far (cache effectiveness)
+        self.pf_replays = 0        # prefill chunk items replayed from a graph (_prefill_graph)
         self.stats: Optional[StepStats] = None
         self.last_stats: Optional[dict] = None
         self.step_events: List[tuple] = []   # stage 0: (step, event) at each step start
@@ -786,22 +793,96 @@ class StageWorker(racecheck.Shared):
     def _prefill(self, gp: GroupPlan, gs: GroupState, inp: Optional[torch.Tensor]):
         st, be, dev = self.stage, self.stage.backend, self.device
         ch = gp.chunks
-        meta = BatchMeta.build([c.slot for c in ch], [c.start for c in ch], [c.qlen for c in ch], dev)
-        if self.first:
-            inp = _h2d([t for c in ch for t in c.ids], torch.int32, dev).to(dev, non_blocking=True)
         finals = [i for i, c in enumerate(ch) if c.final]
         v = gp.g & 1  # alternating-split variant of this group
-        if not self.last:
-            return st.forward(meta, inp, head=False, variant=v)
-        if not finals:
-            st.forward(meta, inp, head=False, variant=v)  # KV cache only
-            return None
-        rows = meta.last_idx.index_select(0, torch.tensor(finals, dtype=torch.long, device=dev))
-        logits = st.forward(meta, inp, head=True, head_rows=rows, variant=v)
+        x, meta = self._prefill_graph(gp, gs, inp, v) if self._prefill_graphs() else (None, None)
+        if x is None:
+            meta = BatchMeta.build([c.slot for c in ch], [c.start for c in ch], [c.qlen for c in ch], dev)
+            if self.first:
+                inp = _h2d([t for c in ch for t in c.ids], torch.int32, dev).to(dev, non_blocking=True)
+            if not self.last:
+                return st.forward(meta, inp, head=False, variant=v)
+            if not finals:
+                st.forward(meta, inp, head=False, variant=v)  # KV cache only
+                return None
+            rows = meta.last_idx.index_select(0, torch.tensor(finals, dtype=torch.long, device=dev))
+            logits = st.forward(meta, inp, head=True, head_rows=rows, variant=v)
+        else:
+            if not self.last:
+                return x
+            if not finals:
+                return None
+            rows = meta.last_idx.index_select(0, torch.tensor(finals, dtype=torch.long, device=dev))
+            be.decode = False
+            logits = st.head(x, meta, rows=rows)
         fc = [ch[i] for i in finals]
         samp = SamplingState([c.temperature for c in fc], [c.top_k for c in fc],
                              [c.greedy for c in fc], [c.seed for c in fc], dev)
         return be.sample(logits, samp, st.cfg.vocab_size)
+
+    # Prefill chunks as hipGraphs (the non-steady items):
+    # a chunk item whose shape (per-sequence query counts, split variant, input
+    # buffer) was seen before replays a captured graph of this stage's forward
+    # instead of issuing its ~10 launches per layer from Python.  The graph's
+    # index tensors (token slots / positions, sequence slots / starts, and on
+    # stage 0 the token ids) are views of ONE device buffer refilled by one
+    # host-to-device copy on the lane before each replay; row offsets and
+    # attention tiles depend on the query counts only and stay fixed.  The
+    # edge transfers stay eager and the last stage's head + sampler run after
+    # the replay.  First use of a shape: eager (workspaces, routing); second:
+    # capture.  "auto" = on with P > 1 stages (the schedule that chunks prompts:
+    # bench.py --prefill-chunk -1), LSD_PREFILL_GRAPHS=1 / 0 forces it.
+    PREFILL_GRAPHS = os.environ.get("LSD_PREFILL_GRAPHS", "auto")
+
+    def _prefill_graphs(self) -> bool:
+        v = self.PREFILL_GRAPHS
+        return (self.use_graphs and self.device.type == "cuda"
+                and (v == "1" or (v == "auto" and self.P > 1)))
+
+    def _prefill_graph(self, gp: GroupPlan, gs: GroupState, inp: Optional[torch.Tensor], v: int):
+        """(hidden out [T, H], static meta) from the chunk's graph, or (None,
+        None): first use of the shape, run eagerly."""
+        ch = gp.chunks
+        qlens = tuple(c.qlen for c in ch)
+        T, B = sum(qlens), len(ch)
+        key = (qlens, v, None if self.first else inp.data_ptr())
+        ent = gs.pf_graphs.get(key)
+        if ent is None and key not in gs.pf_seen:
+            gs.pf_seen.add(key)
+            return None, None
+        dev = self.device
+        vals = ([c.slot for c in ch for _ in range(c.qlen)] + [p for c in ch for p in range(c.start, c.start + c.qlen)]
+                + [c.slot for c in ch] + [c.start for c in ch])
+        if self.first:
+            vals += [t for c in ch for t in c.ids]
+        host = _h2d(vals, torch.int32, dev)
+        if getattr(self.t, "aborted", False):
+            from .comm import TransportError
+
+            raise TransportError("data plane aborted: prefill graph not replayed")
+        if ent is None:
+            buf = torch.empty(len(vals), dtype=torch.int32, device=dev)
+            buf.copy_(host, non_blocking=True)
+            cu = [0]
+            for n in qlens:
+                cu.append(cu[-1] + n)
+            cu_t = torch.tensor(cu, dtype=torch.int32, device=dev)
+            meta = BatchMeta(token_slots=buf[:T], token_pos=buf[T: 2 * T], seq_slots=buf[2 * T: 2 * T + B],
+                             q_start=buf[2 * T + B: 2 * T + 2 * B], cu_q=cu_t, last_idx=cu_t[1:] - 1,
+                             num_tokens=T, num_seqs=B, max_q=max(qlens), max_ctx=0, is_decode=False,
+                             host_qlens=list(qlens))
+            from ..ops.hip import prefill_tiles
+
+            meta._tiles = prefill_tiles(meta).to(dev)
+            x_in = buf[2 * T + 2 * B:] if self.first else inp
+            g, out, _ = self._capture(lambda: self.stage.forward(meta, x_in, head=False, variant=v))
+            ent = gs.pf_graphs[key] = (g, buf, meta, out)
+            self.captures += 1
+        else:
+            ent[1].copy_(host, non_blocking=True)
+        ent[0].replay()
+        self.pf_replays += 1
+        return ent[3], ent[2]
 
     def _decode(self, gp: GroupPlan, gs: GroupState, inp: torch.Tensor, io: bool = False) -> torch.Tensor:
         key = (gp.b, gp.ctxb, io)

@@ -136,6 +136,25 @@ def test_graphs_cached_across_sessions():
     assert sum(w.captures for w in e.workers) == c
 
 
+@pytest.mark.parametrize("chunk", [0, 2, 3])
+def test_prefill_chunk_graphs_bit_identical(monkeypatch, chunk):
+    """Prefill chunks replayed from captured graphs (pipeline.py
+    _prefill_graph, forced on one stage) give the eager path's tokens; the
+    chunk index buffer is refilled per replay (slots and starts differ between
+    the chunks of one shape), the last stage samples after the replay."""
+    from llm_sharding_demo_amd.parallel.pipeline import StageWorker
+
+    sp = SamplingParams(temperature=0.8, top_k=20, seed=5, max_new_tokens=6)
+    prompts = [[i + 1, 2 * i + 3, 5, 7, i + 9, 11] for i in range(8)]
+    monkeypatch.setattr(StageWorker, "PREFILL_GRAPHS", "0")
+    want = _engine("gpt2-test", prefill_chunk=chunk).generate_ids(prompts, sp, microbatches=2)
+    monkeypatch.setattr(StageWorker, "PREFILL_GRAPHS", "1")
+    e = _engine("gpt2-test", prefill_chunk=chunk)
+    for _ in range(3):  # eager, capture, replay
+        assert e.generate_ids(prompts, sp, microbatches=2) == want
+    assert sum(w.pf_replays for w in e.workers) > 0
+
+
 @pytest.mark.parametrize("P,chunk", [(2, 0), (4, 0), (3, 2), (4, 1)])
 def test_loopback_multi_stage_bit_identical(P, chunk):
     """P stage threads on one GPU with the device-async loopback transport
