@@ -844,6 +844,11 @@ class StageWorker(racecheck.Shared):
         None): first use of the shape, run eagerly."""
         ch = gp.chunks
         qlens = tuple(c.qlen for c in ch)
+        if all(n == 1 for n in qlens):
+            # one query per sequence: BatchMeta.build makes this a decode batch
+            # (decode kernels, attention splits sized by the host context
+            # bound) -- eager, as before
+            return None, None
         T, B = sum(qlens), len(ch)
         key = (qlens, v, None if self.first else inp.data_ptr())
         ent = gs.pf_graphs.get(key)

@@ -136,7 +136,7 @@ def test_graphs_cached_across_sessions():
     assert sum(w.captures for w in e.workers) == c
 
 
-@pytest.mark.parametrize("chunk", [0, 2, 3])
+@pytest.mark.parametrize("chunk", [0, 2, 3, 5])
 def test_prefill_chunk_graphs_bit_identical(monkeypatch, chunk):
     """Prefill chunks replayed from captured graphs (pipeline.py
     _prefill_graph, forced on one stage) give the eager path's tokens; the
@@ -145,6 +145,8 @@ def test_prefill_chunk_graphs_bit_identical(monkeypatch, chunk):
     from llm_sharding_demo_amd.parallel.pipeline import StageWorker
 
     sp = SamplingParams(temperature=0.8, top_k=20, seed=5, max_new_tokens=6)
+    # chunk 5: the second chunk has one query per sequence (a decode-shaped
+    # batch, which stays eager)
     prompts = [[i + 1, 2 * i + 3, 5, 7, i + 9, 11] for i in range(8)]
     monkeypatch.setattr(StageWorker, "PREFILL_GRAPHS", "0")
     want = _engine("gpt2-test", prefill_chunk=chunk).generate_ids(prompts, sp, microbatches=2)
