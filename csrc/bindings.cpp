@@ -61,6 +61,7 @@ hipError_t lsd_attn_oproj(const bf16* q, long ldq, const bf16* kc, const bf16* v
 int lsd_gemv_ok(int M, int K, int epi, int norm);
 void lsd_gemv_set_nt(int v);
 hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st);
+hipError_t lsd_silu_mul(const lsd_bf16_t* y, long ldy, lsd_bf16_t* out, long ldo, int M, int F, hipStream_t st);
 hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                       const int* topk, const int* greedy, const long long* seeds,
                       long long* step, int* out, int advance, const int* active, int* pos,
@@ -633,6 +634,19 @@ void sample_launch(const torch::Tensor& logits, int64_t V, const torch::Tensor& 
                        out.data_ptr<int>(), advance ? 1 : 0, act, pp, sm, ldseg, cur_stream()), "sample");
 }
 
+// out[m, 16 j + i] = silu(y[m, 32 j + i]) * y[m, 32 j + 16 + i]: the SiLU * up
+// pass over a gate/up-interleaved GEMM output (elementwise.hip)
+torch::Tensor silu_mul(torch::Tensor y) {
+  need(y, torch::kBFloat16, "y");
+  TORCH_CHECK(y.dim() == 2 && y.stride(1) == 1 && y.size(1) % 32 == 0, "silu_mul: y [M, 2F], 2F % 32 == 0");
+  TORCH_CHECK(y.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0, "silu_mul: 16-byte rows");
+  const int M = y.size(0), F = y.size(1) / 2;
+  auto out = torch::empty({M, F}, y.options());
+  check_hip(lsd_silu_mul(bptr(y), y.stride(0), reinterpret_cast<lsd_bf16_t*>(out.data_ptr()), F, M, F,
+                         cur_stream()), "silu_mul");
+  return out;
+}
+
 torch::Tensor sample(torch::Tensor logits, int64_t V, torch::Tensor temp, torch::Tensor topk,
                      torch::Tensor greedy, torch::Tensor seeds, torch::Tensor step,
                      c10::optional<torch::Tensor> segmax) {
@@ -681,6 +695,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("greedy"), py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("active"),
         py::arg("pos") = py::none(), py::arg("segmax") = py::none());
   m.def("gemv", &gemv);
+  m.def("silu_mul", &silu_mul);
   // GEMV weight stream with non-temporal loads (A/B knob, LSD_GEMV_NT)
   m.def("gemv_set_nt", [](int64_t v) { lsd_gemv_set_nt((int)v); });
   m.def("gemv_ok", [](int64_t M, int64_t K, int64_t epi, int64_t norm) {

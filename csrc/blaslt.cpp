@@ -13,7 +13,9 @@
 // the column-major D[N, M] = op_T(W[K, N]) B[K, M]: transa = T, m = N, n = M.
 // The bias runs along D's rows (our columns) as the epilogue expects.
 //
-// One handle, workspace and heuristic cache per device; the first call of a
+// One handle and heuristic cache per device, a workspace per microbatch lane
+// (the lanes' GEMMs run concurrently; decode calls are graph-captured, and a
+// lane's captures and replays share its workspace); the first call of a
 // (M, N, K, epilogue) asks the heuristic and keeps its first algorithm.
 // The bindings report "no algorithm" (None / false, nothing issued) and the
 // caller then keeps the hand-written kernel.
@@ -46,20 +48,19 @@ struct Plan {
 
 struct DeviceState {
   hipblasLtHandle_t handle = nullptr;
-  torch::Tensor workspace;
+  std::map<int, torch::Tensor> workspace;  // per microbatch lane: lanes run concurrently
   std::map<std::tuple<long, long, long, int, int>, Plan> plans;  // (M, N, K, epilogue, fp32 out)
 };
 
 std::mutex g_mu;
 std::map<int, DeviceState> g_dev;
 
-DeviceState& state(const torch::Tensor& like) {
+DeviceState& state(const torch::Tensor& like, int lane) {
   const int dev = like.get_device();
   auto& s = g_dev[dev];
-  if (!s.handle) {
-    lt_check(hipblasLtCreate(&s.handle), "create");
-    s.workspace = torch::empty({(long)kWorkspace}, like.options().dtype(torch::kUInt8));
-  }
+  if (!s.handle) lt_check(hipblasLtCreate(&s.handle), "create");
+  if (!s.workspace.count(lane))
+    s.workspace[lane] = torch::empty({(long)kWorkspace}, like.options().dtype(torch::kUInt8));
   return s;
 }
 
@@ -114,14 +115,14 @@ const void* bias_ptr(const c10::optional<torch::Tensor>& bias, long N) {
 }
 
 void run(DeviceState& s, Plan& p, const void* bias, const torch::Tensor& a, const torch::Tensor& w,
-         float beta, void* cd) {
+         float beta, void* cd, int lane) {
   if (bias)
     lt_check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)),
              "bias pointer");
   const float alpha = 1.f;
   auto st = at::hip::getCurrentHIPStream().stream();
   lt_check(hipblasLtMatmul(s.handle, p.desc, &alpha, w.data_ptr(), p.la, a.data_ptr(), p.lb, &beta, cd, p.lc, cd,
-                           p.lc, &p.algo, s.workspace.data_ptr(), kWorkspace, st),
+                           p.lc, &p.algo, s.workspace.at(lane).data_ptr(), kWorkspace, st),
            "matmul");
 }
 
@@ -131,7 +132,7 @@ void lsd_register_blaslt(pybind11::module& m) {
   // y = act(a @ w^T + bias), bf16 [M, N]; act 0 none, 1 GELU.  None when the
   // library has no algorithm for the shape (use the hand-written kernel)
   m.def("blaslt_linear", [](torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,
-                            int64_t act) -> c10::optional<torch::Tensor> {
+                            int64_t act, int64_t lane) -> c10::optional<torch::Tensor> {
     check_operands(a, w);
     const c10::DeviceGuard guard(a.device());
     TORCH_CHECK(act == 0 || act == 1, "blaslt_linear: act 0 (none) or 1 (GELU)");
@@ -140,17 +141,17 @@ void lsd_register_blaslt(pybind11::module& m) {
     const hipblasLtEpilogue_t epi = act == 1 ? (b ? HIPBLASLT_EPILOGUE_GELU_BIAS : HIPBLASLT_EPILOGUE_GELU)
                                              : (b ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT);
     std::lock_guard<std::mutex> lk(g_mu);
-    auto& s = state(a);
+    auto& s = state(a, (int)lane);
     auto& p = plan(s, M, N, K, epi, false);
     if (!p.ok) return c10::nullopt;
     auto y = torch::empty({M, N}, a.options());
-    run(s, p, b, a, w, 0.f, y.data_ptr());
+    run(s, p, b, a, w, 0.f, y.data_ptr(), (int)lane);
     return y;
-  }, py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("act"));
+  }, py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("lane") = 0);
   // x += a @ w^T + bias (x fp32 [M, N], in place); false when the library has
   // no algorithm for the shape (nothing was issued)
   m.def("blaslt_residual", [](torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,
-                              torch::Tensor x) -> bool {
+                              torch::Tensor x, int64_t lane) -> bool {
     check_operands(a, w);
     const c10::DeviceGuard guard(a.device());
     const long M = a.size(0), N = w.size(0), K = a.size(1);
@@ -161,10 +162,10 @@ void lsd_register_blaslt(pybind11::module& m) {
     if (bias.has_value()) b32 = bias->to(torch::kFloat32);
     const void* b = bias.has_value() ? b32.data_ptr() : nullptr;
     std::lock_guard<std::mutex> lk(g_mu);
-    auto& s = state(a);
+    auto& s = state(a, (int)lane);
     auto& p = plan(s, M, N, K, b ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT, true);
     if (!p.ok) return false;
-    run(s, p, b, a, w, 1.f, x.data_ptr());
+    run(s, p, b, a, w, 1.f, x.data_ptr(), (int)lane);
     return true;
-  }, py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("x"));
+  }, py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("x"), py::arg("lane") = 0);
 }

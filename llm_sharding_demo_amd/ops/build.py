@@ -27,7 +27,7 @@ BUILD = os.path.join(ROOT, "build", "native")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-KERNELS = ["gemm.hip", "gemv.hip", "norm.hip", "attention.hip", "sample.hip", "loopback.hip"]
+KERNELS = ["gemm.hip", "gemv.hip", "norm.hip", "attention.hip", "sample.hip", "loopback.hip", "elementwise.hip"]
 # host code of the extension: kernel bindings, native RCCL communicator, native stage
 # executor, device loopback channels (single-GPU rehearsal of the RCCL edges),
 # hipBLASLt prefill projections

@@ -142,6 +142,11 @@ class HipBackend(Backend):
     BLASLT_MIN_M = int(os.environ.get("LSD_BLASLT_MIN_M", "4096"))
     BLASLT_RESID_MIN_K = int(os.environ.get("LSD_BLASLT_RESID_MIN_K", "4096"))
     BLASLT_GELU_MIN_M = int(os.environ.get("LSD_BLASLT_GELU_MIN_M", "65536"))
+    # decode gate_up (SiLU * up) from this many rows: the hipBLASLt GEMM, then
+    # the elementwise pass (elementwise.hip) -- Llama-3 8B at 512 rows 132 ->
+    # 109 + ~8 us (tools/bench_llama_blaslt.py, profiles/r5_llama_blaslt.log;
+    # a tie at 256 rows, where the fused ring kernel stays).  0 = off
+    BLASLT_SILU_MIN_M = int(os.environ.get("LSD_BLASLT_SILU_MIN_M", "512"))
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
     # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:
@@ -520,9 +525,14 @@ class HipBackend(Backend):
         a = self.materialize(a)
         if code == 1 and self._blaslt(a.shape[0]) and a.shape[0] >= self.BLASLT_GELU_MIN_M \
                 and a.is_contiguous():
-            y = self.C.blaslt_linear(a, w, b, code)
+            y = self.C.blaslt_linear(a, w, b, code, self.lane)
             if y is not None:
                 return y
+        if code == 2 and self.BLASLT_SILU_MIN_M and a.shape[0] >= self.BLASLT_SILU_MIN_M \
+                and getattr(self, "decode", False) and a.is_contiguous() and w.shape[0] % 32 == 0:
+            y = self.C.blaslt_linear(a, w, b, 0, self.lane)
+            if y is not None:
+                return self.C.silu_mul(y)
         tiled, splits = self._gemm_kw(a.shape[0], w.shape[0], w.shape[1], 2 if code == 2 else 1)
         return self.C.linear(a, w, b, code, tiled, splits, self.counters)
 
@@ -537,7 +547,7 @@ class HipBackend(Backend):
                         0, 0, 0, None)
             return
         if self._blaslt(M) and K >= self.BLASLT_RESID_MIN_K and a.is_contiguous() \
-                and self.C.blaslt_residual(a, w, b, r.x):
+                and self.C.blaslt_residual(a, w, b, r.x, self.lane):
             return
         splits = self._resid_splits(M, N, K)
         tiled = self._tiled(M, N)

@@ -653,6 +653,24 @@ def test_blaslt_prefill_projections(C, M, N, K):
         close(x, x_ref, 2e-3, 1e-3)
 
 
+@pytest.mark.parametrize("M", [512, 100])
+def test_silu_mul_after_blaslt(C, CNT, M):
+    """Decode gate_up at >= 512 rows: the hipBLASLt GEMM over the
+    gate/up-interleaved weight, then the SiLU*up pass (elementwise.hip) --
+    against the fp32 reference and the fused-epilogue kernel."""
+    from llm_sharding_demo_amd.ops.hip import interleave_gate_up
+
+    F, K = 1024, 512
+    a, w = bf(M, K, seed=98), bf(2 * F, K, scale=0.05, seed=99)
+    wi = interleave_gate_up(w, F).contiguous()
+    y = C.blaslt_linear(a, wi, None, 0)
+    assert y is not None
+    out = C.silu_mul(y)
+    ref_out = ref.silu_mul(*ref.linear(a, w).split(F, 1))
+    close(out, ref_out, 3e-2)
+    close(out, C.linear(a, wi, None, 2, True, 1, CNT), 3e-2)
+
+
 def _segmax(logits):
     """What linear_f32 writes beside these logits (padding columns included)."""
     B, Vp = logits.shape

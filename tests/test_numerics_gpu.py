@@ -86,3 +86,18 @@ def test_headline_decode_shape_matches_fp32_golden():
     assert gate(r), r
     assert not gate(r3), r3
     torch.cuda.empty_cache()
+
+
+def test_llama_512_row_decode_matches_fp32_golden():
+    """Llama-3 8B dims (4 layers) with 512 sequences: the 512-row decode
+    gate_up runs on hipBLASLt followed by the SiLU*up pass (ops/hip.py
+    BLASLT_SILU_MIN_M) -- against the fp32 golden with the Llama bounds."""
+    from llm_sharding_demo_amd.config import get_model_config
+
+    mc = dataclasses.replace(get_model_config("llama-3-8b"), n_layers=4)
+    prompts = _prompts(mc.vocab_size, [12] * 512, seed=13)
+    r, r3 = compare_with_golden(mc, prompts, steps=3, inject=(1.0, 3.0))
+    print("llama-3-8b 512 rows", r)
+    assert _gate("llama-3-8b", r), r
+    assert not _gate("llama-3-8b", r3), r3
+    torch.cuda.empty_cache()
