@@ -143,10 +143,12 @@ class HipBackend(Backend):
     BLASLT_RESID_MIN_K = int(os.environ.get("LSD_BLASLT_RESID_MIN_K", "4096"))
     BLASLT_GELU_MIN_M = int(os.environ.get("LSD_BLASLT_GELU_MIN_M", "65536"))
     # decode gate_up (SiLU * up) from this many rows: the hipBLASLt GEMM, then
-    # the elementwise pass (elementwise.hip) -- Llama-3 8B at 512 rows 132 ->
-    # 109 + ~8 us (tools/bench_llama_blaslt.py, profiles/r5_llama_blaslt.log;
-    # a tie at 256 rows, where the fused ring kernel stays).  0 = off
-    BLASLT_SILU_MIN_M = int(os.environ.get("LSD_BLASLT_SILU_MIN_M", "512"))
+    # the elementwise pass (elementwise.hip).  Alone, Llama-3 8B at 512 rows
+    # 132 -> 109 + ~8 us (tools/bench_llama_blaslt.py), but the 512-sequence
+    # bench lost 1-1.5 % with it (30.9 / 30.7k vs 31.2 / 31.1k tok/s,
+    # profiles/r5_llama_blaslt.log): off (0) by default, LSD_BLASLT_SILU_MIN_M
+    # turns it on
+    BLASLT_SILU_MIN_M = int(os.environ.get("LSD_BLASLT_SILU_MIN_M", "0"))
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
     # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:
