@@ -833,6 +833,10 @@ class StageWorker(racecheck.Shared):
     # capture.  "auto" = on with P > 1 stages (the schedule that chunks prompts:
     # bench.py --prefill-chunk -1), LSD_PREFILL_GRAPHS=1 / 0 forces it.
     PREFILL_GRAPHS = os.environ.get("LSD_PREFILL_GRAPHS", "auto")
+    # captured prefill graphs kept per group (each holds its activations'
+    # memory pool): serving with varied prompt mixes would otherwise grow them
+    # without bound; the oldest is dropped first
+    PREFILL_GRAPHS_MAX = int(os.environ.get("LSD_PREFILL_GRAPHS_MAX", "16"))
 
     def _prefill_graphs(self) -> bool:
         v = self.PREFILL_GRAPHS
@@ -853,6 +857,8 @@ class StageWorker(racecheck.Shared):
         key = (qlens, v, None if self.first else inp.data_ptr())
         ent = gs.pf_graphs.get(key)
         if ent is None and key not in gs.pf_seen:
+            if len(gs.pf_seen) >= 64 * self.PREFILL_GRAPHS_MAX:
+                gs.pf_seen.clear()  # shapes seen once long ago: forget them
             gs.pf_seen.add(key)
             return None, None
         dev = self.device
@@ -866,6 +872,11 @@ class StageWorker(racecheck.Shared):
 
             raise TransportError("data plane aborted: prefill graph not replayed")
         if ent is None:
+            while gs.pf_graphs and len(gs.pf_graphs) >= max(1, self.PREFILL_GRAPHS_MAX):
+                # a replay of the oldest graph may still be in flight on this
+                # lane: let it finish before its memory pool is released
+                torch.cuda.current_stream(dev).synchronize()
+                gs.pf_graphs.pop(next(iter(gs.pf_graphs)))
             buf = torch.empty(len(vals), dtype=torch.int32, device=dev)
             buf.copy_(host, non_blocking=True)
             cu = [0]

@@ -171,6 +171,25 @@ def test_prefill_chunk_graphs_bit_identical(monkeypatch, chunk):
     assert sum(w.pf_replays for w in e.workers) > 0
 
 
+def test_prefill_graphs_bounded(monkeypatch):
+    """Serving with changing prompt mixes: at most PREFILL_GRAPHS_MAX prefill
+    graphs stay captured per group (oldest dropped), tokens unchanged."""
+    from llm_sharding_demo_amd.parallel.pipeline import StageWorker
+
+    sp = SamplingParams(greedy=True, max_new_tokens=3)
+    mixes = [[[j + 1] * (3 + (k + j) % 4) for j in range(4)] for k in range(6)]
+    monkeypatch.setattr(StageWorker, "PREFILL_GRAPHS", "0")
+    want = [_engine("gpt2-test").generate_ids(m, sp) for m in mixes]
+    monkeypatch.setattr(StageWorker, "PREFILL_GRAPHS", "1")
+    monkeypatch.setattr(StageWorker, "PREFILL_GRAPHS_MAX", 2)
+    e = _engine("gpt2-test")
+    for _ in range(3):
+        for m, w in zip(mixes, want):
+            assert e.generate_ids(m, sp) == w
+    assert sum(w.pf_replays for w in e.workers) > 0
+    assert all(len(gs.pf_graphs) <= 2 for w in e.workers for gs in w.groups.values())
+
+
 @pytest.mark.parametrize("P,chunk", [(2, 0), (4, 0), (3, 2), (4, 1)])
 def test_loopback_multi_stage_bit_identical(P, chunk):
     """P stage threads on one GPU with the device-async loopback transport
