@@ -32,11 +32,13 @@ from __future__ import annotations
 
 import contextlib
 import gc
+import itertools
 import os
 import threading
 import time
 from typing import Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 
 from ..models.stage import StageModel
@@ -212,6 +214,8 @@ class GroupState(racecheck.Shared):
         # -> (graph, packed index buffer, static meta, output); see _prefill_graph
         self.pf_graphs: Dict[tuple, tuple] = {}
         self.pf_seen: set = set()
+        self.pf_pin: List[list] = []  # [pinned int32 staging, event of its last copy] ring
+        self.pf_pin_next = 0
         self._metas: Dict[tuple, BatchMeta] = {}
         self.rows_n = 0
 
@@ -862,11 +866,7 @@ class StageWorker(racecheck.Shared):
             gs.pf_seen.add(key)
             return None, None
         dev = self.device
-        vals = ([c.slot for c in ch for _ in range(c.qlen)] + [p for c in ch for p in range(c.start, c.start + c.qlen)]
-                + [c.slot for c in ch] + [c.start for c in ch])
-        if self.first:
-            vals += [t for c in ch for t in c.ids]
-        host = _h2d(vals, torch.int32, dev)
+        arr = _chunk_index(ch, qlens, self.first)
         if getattr(self.t, "aborted", False):
             from .comm import TransportError
 
@@ -877,8 +877,8 @@ class StageWorker(racecheck.Shared):
                 # lane: let it finish before its memory pool is released
                 torch.cuda.current_stream(dev).synchronize()
                 gs.pf_graphs.pop(next(iter(gs.pf_graphs)))
-            buf = torch.empty(len(vals), dtype=torch.int32, device=dev)
-            buf.copy_(host, non_blocking=True)
+            buf = torch.empty(arr.size, dtype=torch.int32, device=dev)
+            self._stage_h2d(gs, arr, buf)
             cu = [0]
             for n in qlens:
                 cu.append(cu[-1] + n)
@@ -895,10 +895,33 @@ class StageWorker(racecheck.Shared):
             ent = gs.pf_graphs[key] = (g, buf, meta, out)
             self.captures += 1
         else:
-            ent[1].copy_(host, non_blocking=True)
+            self._stage_h2d(gs, arr, ent[1])
         ent[0].replay()
         self.pf_replays += 1
         return ent[3], ent[2]
+
+    _PF_PIN = 4  # staging buffers per group: a copy's source is reused 4 chunks later
+
+    def _stage_h2d(self, gs: GroupState, arr: np.ndarray, dst: torch.Tensor) -> None:
+        """Host int32 array -> dst (device), through a ring of pinned staging
+        buffers owned by the group (no per-call pinned allocation: under
+        several stage threads, torch's pin_memory took ~1 ms a call,
+        profiles/r5_profile_issue.log); a buffer is reused only after the
+        copy out of it has completed (its event)."""
+        n = arr.size
+        if len(gs.pf_pin) < self._PF_PIN:
+            gs.pf_pin.append([torch.empty(max(n, 1 << 12), dtype=torch.int32, pin_memory=True),
+                              torch.cuda.Event(), False])
+        slot = gs.pf_pin[gs.pf_pin_next % len(gs.pf_pin)]
+        gs.pf_pin_next += 1
+        if slot[2]:
+            slot[1].synchronize()
+        if slot[0].numel() < n:
+            slot[0] = torch.empty(2 * n, dtype=torch.int32, pin_memory=True)
+        slot[0].numpy()[:n] = arr
+        dst.copy_(slot[0][:n], non_blocking=True)
+        slot[1].record()
+        slot[2] = True
 
     def _decode(self, gp: GroupPlan, gs: GroupState, inp: torch.Tensor, io: bool = False) -> torch.Tensor:
         key = (gp.b, gp.ctxb, io)
@@ -1035,6 +1058,23 @@ def _cu_masked_lanes(dev: torch.device, n: int, mode: str) -> List[torch.cuda.Ex
                 mask[c // 32] |= 1 << (c % 32)
             lanes.append(torch.cuda.ExternalStream(C.stream_with_cu_mask(mask), device=dev))
     return lanes
+
+
+def _chunk_index(ch, qlens, first: bool) -> np.ndarray:
+    """A prefill chunk item's index buffer, int32: token slots [T], token
+    positions [T], sequence slots [B], sequence starts [B] (and on stage 0
+    the token ids [T]) -- vectorised (a 256 x 32-token item is 16-24 K values)."""
+    B = len(ch)
+    q = np.asarray(qlens, dtype=np.int64)
+    T = int(q.sum())
+    sl = np.fromiter((c.slot for c in ch), dtype=np.int64, count=B)
+    st = np.fromiter((c.start for c in ch), dtype=np.int64, count=B)
+    cu = np.zeros(B + 1, dtype=np.int64)
+    np.cumsum(q, out=cu[1:])
+    parts = [np.repeat(sl, q), np.arange(T, dtype=np.int64) + np.repeat(st - cu[:-1], q), sl, st]
+    if first:
+        parts.append(np.fromiter(itertools.chain.from_iterable(c.ids for c in ch), dtype=np.int64, count=T))
+    return np.concatenate(parts).astype(np.int32)
 
 
 def _h2d(vals, dtype, dev) -> torch.Tensor:
