@@ -801,9 +801,9 @@ class StageWorker(racecheck.Shared):
         v = gp.g & 1  # alternating-split variant of this group
         x, meta = self._prefill_graph(gp, gs, inp, v) if self._prefill_graphs() else (None, None)
         if x is None:
-            meta = BatchMeta.build([c.slot for c in ch], [c.start for c in ch], [c.qlen for c in ch], dev)
+            meta, ids, _ = self._chunk_meta(gs, ch, tuple(c.qlen for c in ch))
             if self.first:
-                inp = _h2d([t for c in ch for t in c.ids], torch.int32, dev).to(dev, non_blocking=True)
+                inp = ids
             if not self.last:
                 return st.forward(meta, inp, head=False, variant=v)
             if not finals:
@@ -857,7 +857,6 @@ class StageWorker(racecheck.Shared):
             # (decode kernels, attention splits sized by the host context
             # bound) -- eager, as before
             return None, None
-        T, B = sum(qlens), len(ch)
         key = (qlens, v, None if self.first else inp.data_ptr())
         ent = gs.pf_graphs.get(key)
         if ent is None and key not in gs.pf_seen:
@@ -866,7 +865,6 @@ class StageWorker(racecheck.Shared):
             gs.pf_seen.add(key)
             return None, None
         dev = self.device
-        arr = _chunk_index(ch, qlens, self.first)
         if getattr(self.t, "aborted", False):
             from .comm import TransportError
 
@@ -877,28 +875,44 @@ class StageWorker(racecheck.Shared):
                 # lane: let it finish before its memory pool is released
                 torch.cuda.current_stream(dev).synchronize()
                 gs.pf_graphs.pop(next(iter(gs.pf_graphs)))
-            buf = torch.empty(arr.size, dtype=torch.int32, device=dev)
-            self._stage_h2d(gs, arr, buf)
-            cu = [0]
-            for n in qlens:
-                cu.append(cu[-1] + n)
-            cu_t = torch.tensor(cu, dtype=torch.int32, device=dev)
-            meta = BatchMeta(token_slots=buf[:T], token_pos=buf[T: 2 * T], seq_slots=buf[2 * T: 2 * T + B],
-                             q_start=buf[2 * T + B: 2 * T + 2 * B], cu_q=cu_t, last_idx=cu_t[1:] - 1,
-                             num_tokens=T, num_seqs=B, max_q=max(qlens), max_ctx=0, is_decode=False,
-                             host_qlens=list(qlens))
+            meta, ids, buf = self._chunk_meta(gs, ch, qlens)
             from ..ops.hip import prefill_tiles
 
             meta._tiles = prefill_tiles(meta).to(dev)
-            x_in = buf[2 * T + 2 * B:] if self.first else inp
+            x_in = ids if self.first else inp
             g, out, _ = self._capture(lambda: self.stage.forward(meta, x_in, head=False, variant=v))
             ent = gs.pf_graphs[key] = (g, buf, meta, out)
             self.captures += 1
         else:
-            self._stage_h2d(gs, arr, ent[1])
+            self._chunk_meta(gs, ch, qlens, ent[1])
         ent[0].replay()
         self.pf_replays += 1
         return ent[3], ent[2]
+
+    def _chunk_meta(self, gs: GroupState, ch, qlens, buf: Optional[torch.Tensor] = None):
+        """(BatchMeta, stage 0's token ids or None, index buffer) of a prefill
+        chunk item: every index tensor is a view of ONE device buffer filled by
+        one staged host-to-device copy (`buf` given: refill that one).  The
+        same values as BatchMeta.build, including a decode-shaped batch (one
+        query per sequence)."""
+        dev = self.device
+        T, B = sum(qlens), len(ch)
+        if dev.type != "cuda":
+            meta = BatchMeta.build([c.slot for c in ch], [c.start for c in ch], list(qlens), dev)
+            ids = (_h2d([t for c in ch for t in c.ids], torch.int32, dev).to(dev) if self.first else None)
+            return meta, ids, None
+        arr = _chunk_index(ch, qlens, self.first)
+        if buf is None:
+            buf = torch.empty(arr.size, dtype=torch.int32, device=dev)
+        self._stage_h2d(gs, arr, buf)
+        o = 2 * T + 2 * B
+        dec = all(n == 1 for n in qlens)
+        meta = BatchMeta(token_slots=buf[:T], token_pos=buf[T: 2 * T], seq_slots=buf[2 * T: 2 * T + B],
+                         q_start=buf[2 * T + B: o], cu_q=buf[o: o + B + 1], last_idx=buf[o + B + 1: o + 2 * B + 1],
+                         num_tokens=T, num_seqs=B, max_q=max(qlens, default=0),
+                         max_ctx=max((c.start + n for c, n in zip(ch, qlens)), default=0), is_decode=dec,
+                         host_qlens=list(qlens))
+        return meta, (buf[o + 2 * B + 1:] if self.first else None), buf
 
     _PF_PIN = 4  # staging buffers per group: a copy's source is reused 4 chunks later
 
@@ -1062,8 +1076,9 @@ def _cu_masked_lanes(dev: torch.device, n: int, mode: str) -> List[torch.cuda.Ex
 
 def _chunk_index(ch, qlens, first: bool) -> np.ndarray:
     """A prefill chunk item's index buffer, int32: token slots [T], token
-    positions [T], sequence slots [B], sequence starts [B] (and on stage 0
-    the token ids [T]) -- vectorised (a 256 x 32-token item is 16-24 K values)."""
+    positions [T], sequence slots [B], sequence starts [B], row offsets
+    [B + 1], last rows [B] (and on stage 0 the token ids [T]) -- vectorised
+    (a 256 x 32-token item is 16-24 K values)."""
     B = len(ch)
     q = np.asarray(qlens, dtype=np.int64)
     T = int(q.sum())
@@ -1071,7 +1086,7 @@ def _chunk_index(ch, qlens, first: bool) -> np.ndarray:
     st = np.fromiter((c.start for c in ch), dtype=np.int64, count=B)
     cu = np.zeros(B + 1, dtype=np.int64)
     np.cumsum(q, out=cu[1:])
-    parts = [np.repeat(sl, q), np.arange(T, dtype=np.int64) + np.repeat(st - cu[:-1], q), sl, st]
+    parts = [np.repeat(sl, q), np.arange(T, dtype=np.int64) + np.repeat(st - cu[:-1], q), sl, st, cu, cu[1:] - 1]
     if first:
         parts.append(np.fromiter(itertools.chain.from_iterable(c.ids for c in ch), dtype=np.int64, count=T))
     return np.concatenate(parts).astype(np.int32)
