@@ -775,6 +775,9 @@ class StageWorker(racecheck.Shared):
         if b == 0:
             return
         gs.rows_n = n
+        if dev.type == "cuda":
+            self._apply_rows_staged(gs, rows, b, pad, sl, pos, act)
+            return
         gs.slots[:b].copy_(_h2d(sl, torch.int32, dev), non_blocking=True)
         gs.pos[:b].copy_(_h2d(pos, torch.int32, dev), non_blocking=True)
         gs.active[:b].copy_(_h2d(act, torch.int32, dev), non_blocking=True)
@@ -792,6 +795,45 @@ class StageWorker(racecheck.Shared):
         if self.first:
             src = _h2d([r.src for r in rows] + [0] * pad, torch.int64, dev)
             gathered = gs.tin.index_select(0, src.to(dev, non_blocking=True))
+            gs.tin[:b].copy_(gathered)
+
+    def _apply_rows_staged(self, gs: GroupState, rows, b: int, pad: int, sl, pos, act) -> None:
+        """_apply_rows on a GPU: every per-row field packed into ONE int32
+        buffer (float32 temperatures as their bits, int64 seeds / steps as
+        int32 pairs at an even offset) uploaded through the group's pinned
+        staging ring, then device copies into the row state -- instead of one
+        pinned host tensor per field (profiles/r5_profile_issue.log).  The
+        int64 fields start at int32 offset 6 b, so their views are aligned."""
+        i32 = np.int32
+        parts = [np.asarray(sl, i32), np.asarray(pos, i32), np.asarray(act, i32)]
+        if self.last:
+            parts += [np.asarray([r.temperature for r in rows] + [1.0] * pad, np.float32).view(i32),
+                      np.asarray([r.top_k for r in rows] + [1] * pad, i32),
+                      np.asarray([1 if r.greedy else 0 for r in rows] + [1] * pad, i32)]
+            # the int64 fields start at int32 offset 6 b: 8-byte aligned
+            parts += [np.asarray([r.seed for r in rows] + [0] * pad, np.int64).view(i32),
+                      np.asarray([r.step for r in rows] + [0] * pad, np.int64).view(i32)]
+        if self.first:
+            parts.append(np.asarray([r.src for r in rows] + [0] * pad, i32))
+        arr = np.concatenate(parts)
+        buf = getattr(gs, "_rows_buf", None)
+        if buf is None or buf.numel() < arr.size:
+            buf = gs._rows_buf = torch.empty(2 * arr.size, dtype=torch.int32, device=self.device)
+        self._stage_h2d(gs, arr, buf)
+        gs.slots[:b].copy_(buf[:b])
+        gs.pos[:b].copy_(buf[b: 2 * b])
+        gs.active[:b].copy_(buf[2 * b: 3 * b])
+        o = 3 * b
+        if self.last:
+            gs.temp[:b].copy_(buf[o: o + b].view(torch.float32))
+            gs.topk[:b].copy_(buf[o + b: o + 2 * b])
+            gs.greedy[:b].copy_(buf[o + 2 * b: o + 3 * b])
+            o += 3 * b
+            gs.seeds[:b].copy_(buf[o: o + 2 * b].view(torch.int64))
+            gs.sstep[:b].copy_(buf[o + 2 * b: o + 4 * b].view(torch.int64))
+            o += 4 * b
+        if self.first:
+            gathered = gs.tin.index_select(0, buf[o: o + b])
             gs.tin[:b].copy_(gathered)
 
     def _prefill(self, gp: GroupPlan, gs: GroupState, inp: Optional[torch.Tensor]):
