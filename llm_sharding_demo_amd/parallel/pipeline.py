@@ -819,7 +819,7 @@ class StageWorker(racecheck.Shared):
         buf = getattr(gs, "_rows_buf", None)
         if buf is None or buf.numel() < arr.size:
             buf = gs._rows_buf = torch.empty(2 * arr.size, dtype=torch.int32, device=self.device)
-        self._stage_h2d(gs, arr, buf)
+        self._stage_h2d(gs, arr, buf[: arr.size])
         gs.slots[:b].copy_(buf[:b])
         gs.pos[:b].copy_(buf[b: 2 * b])
         gs.active[:b].copy_(buf[2 * b: 3 * b])
