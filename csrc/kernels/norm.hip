@@ -166,6 +166,92 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const void* __restr
   }
 }
 
+// Wave-per-row norm for prefill-sized row counts (no slabs to fold, no row
+// gather): 4 rows per 256-thread block, a row's 16-byte chunks spread over
+// its wave's 64 lanes and all issued before the first use, the statistics
+// merged inside the wave (DPP / permlane butterflies: no LDS, no barrier).
+// Up to 32 rows in flight per CU where the block kernel above holds 8 (2048
+// threads / 256 per row): GPT-2 XL prefill, 32 K rows x 1600, the block
+// kernel streams ~4.5 TB/s (profiles/r4_rejected_norm_loop.log).  A wave per
+// row was slower at decode sizes (profiles/r2_rejected_norm_wave.log), so it
+// only takes T >= lsd_norm_set_wave_min rows.
+template <int MAXC, bool RMS>
+__global__ __launch_bounds__(256) void norm_wave_kernel(const float* __restrict__ x, const bf16* __restrict__ w,
+                                                        const bf16* __restrict__ b, bf16* __restrict__ out,
+                                                        int T, int H, float eps) {
+  const int lane = lane_id();
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= T) return;  // wave-uniform
+  const float* xr = x + (long)row * H;
+  const int nch = H >> 2;  // 16-byte chunks of the row
+  f32x4 v[MAXC];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) v[i] = *reinterpret_cast<const f32x4*>(xr + 4 * min(lane + i * 64, nch - 1));
+  bf16x4 wv[MAXC], bv[MAXC];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = 4 * min(lane + i * 64, nch - 1);
+    wv[i] = ld4(w + c);
+    if (!RMS) bv[i] = ld4(b + c);
+  }
+  float mean = 0.f, var;
+  if (RMS) {
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i)
+      if (lane + i * 64 < nch) s2 += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
+    s2 += wave_xchg<1>(s2);
+    s2 += wave_xchg<2>(s2);
+    s2 += wave_xchg<4>(s2);
+    s2 += wave_xchg<8>(s2);
+    s2 += wave_xchg<16>(s2);
+    s2 += wave_xchg<32>(s2);
+    var = s2 / H;
+  } else {
+    float cnt = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i)
+      if (lane + i * 64 < nch) {
+        cnt += 4.f;
+        s1 += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+      }
+    const float mt = cnt > 0.f ? s1 / cnt : 0.f;
+    float m2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i)
+      if (lane + i * 64 < nch) {
+        const f32x4 d = v[i] - mt;
+        m2 += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+      }
+    Wf st{cnt, mt, m2};
+    st = wf_merge(st, wf_xchg<1>(st));
+    st = wf_merge(st, wf_xchg<2>(st));
+    st = wf_merge(st, wf_xchg<4>(st));
+    st = wf_merge(st, wf_xchg<8>(st));
+    st = wf_merge(st, wf_xchg<16>(st));
+    st = wf_merge(st, wf_xchg<32>(st));
+    mean = st.m;
+    var = st.M / H;
+  }
+  const float rstd = rsqrtf(var + eps);
+  bf16* o = out + (long)row * H;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + i * 64;
+    if (c < nch) {
+      const f32x4 y = (v[i] - mean) * rstd;
+      bf16x4 r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float z = y[j] * bf2f(wv[i][j]);
+        if (!RMS) z += bf2f(bv[i][j]);
+        r[j] = f2bf(z);
+      }
+      st4(o + 4 * c, r);
+    }
+  }
+}
+
 }  // namespace lsd
 
 using namespace lsd;
@@ -177,11 +263,30 @@ extern "C" hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte,
   return hipGetLastError();
 }
 
+static int g_norm_wave_min = 0;  // lsd_norm_set_wave_min(): wave-per-row kernel from this many rows (0 = off)
+extern "C" void lsd_norm_set_wave_min(int v) { g_norm_wave_min = v; }
+
 extern "C" hipError_t lsd_norm(float* x, const void* slab, int slab_bf16, int splits, const bf16* pbias,
                                const bf16* w, const bf16* b, bf16* out, int T, int H, float eps,
                                int rms, const int* rows, int nrows, hipStream_t st) {
   const int n = rows ? nrows : T;
   if (n == 0) return hipSuccess;
+  if (g_norm_wave_min > 0 && T >= g_norm_wave_min && !slab && !rows && out && H % 4 == 0 && H <= 4096) {
+    const int nch = H / 4;
+    const dim3 g((T + 3) / 4), bl(256);
+#define LSD_NORM_W(MC)                                                                         \
+  if (rms) hipLaunchKernelGGL((norm_wave_kernel<MC, true>), g, bl, 0, st, x, w, b, out, T, H, eps); \
+  else hipLaunchKernelGGL((norm_wave_kernel<MC, false>), g, bl, 0, st, x, w, b, out, T, H, eps);
+    if (nch <= 256) {
+      LSD_NORM_W(4)
+    } else if (nch <= 512) {
+      LSD_NORM_W(8)
+    } else {
+      LSD_NORM_W(16)
+    }
+#undef LSD_NORM_W
+    return hipGetLastError();
+  }
   const int maxv = (H + 1023) / 1024;
 #define LSD_NORM_T(MV, S, SB)                                                                     \
   if (rms)                                                                                        \

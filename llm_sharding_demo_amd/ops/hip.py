@@ -227,6 +227,9 @@ class HipBackend(Backend):
     # (p50 8.72 ms: 96 KiB of LDS per workgroup), so 3 slots.
     RING8 = int(os.environ.get("LSD_RING8", "2"))
     RING8_FLAGS = int(os.environ.get("LSD_RING8_FLAGS", "0"))  # A/B bits (gemm.hip)
+    # norms of at least this many rows (prefill) run one wave per row
+    # (norm.hip norm_wave_kernel); 0 = the block-per-row kernel everywhere
+    NORM_WAVE_MIN = int(os.environ.get("LSD_NORM_WAVE_MIN", "0"))
     # lm_head epilogue writes 8-logit segment maxima for the sampler (sample.hip)
     SEGMAX = int(os.environ.get("LSD_SEGMAX", "1"))
     # K splits of the non-residual decode GEMMs on the 8-wave ring (QKV, MLP-up,
@@ -246,6 +249,7 @@ class HipBackend(Backend):
         self.C.gemm_set_d256_slots(self.D256_SLOTS)
         self.C.gemm_set_ring8(self.RING8)
         self.C.gemm_set_ring8_flags(self.RING8_FLAGS)
+        self.C.norm_set_wave_min(self.NORM_WAVE_MIN)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))

@@ -58,6 +58,27 @@ def test_norm_with_slab_combine(C, H, rms, S, sdt):
     close(y2, y_ref[rows.long()], 2e-2)
 
 
+@pytest.mark.parametrize("H", [768, 1600, 4096, 1036])
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("T", [5, 4099])
+def test_norm_wave_per_row(C, H, rms, T):
+    """Prefill norms at >= lsd_norm_set_wave_min rows run one wave per row
+    (norm.hip norm_wave_kernel; forced on here from 1 row): against the fp32
+    reference, odd row counts (a partial last block of 4 rows) and an H whose
+    16-byte chunks do not fill the lanes evenly; x is left untouched."""
+    C.norm_set_wave_min(1)
+    try:
+        x = torch.randn(T, H, device=DEV) * 2 + 0.5
+        x0 = x.clone()
+        w, b = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16(), bf(H, scale=0.1, seed=5)
+        y = C.norm(x, None, None, w, None if rms else b, 1e-5, rms, None, True)
+        y_ref = ref.rmsnorm(x, w, 1e-5) if rms else ref.layernorm(x, w, b, 1e-5)
+        close(y, y_ref, 2e-2)
+        assert torch.equal(x, x0)
+    finally:
+        C.norm_set_wave_min(0)
+
+
 @pytest.fixture(scope="module")
 def CNT():
     return torch.zeros(1 << 16, dtype=torch.int32, device=DEV)

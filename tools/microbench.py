@@ -698,6 +698,13 @@ def main():
     if "p8prof" in which:  # LSD_P8_PROF build: loop cycles split into vmcnt waits and the two barriers
         stamps_p8(act=0)
         stamps_p8(M=4096, N=4096, K=4096, act=0)
+    if "normwave" in which:  # prefill norms: block per row vs wave per row
+        for T, H in ((8192, 1600), (32768, 1600), (65536, 1600), (8192, 4096), (32768, 768)):
+            for wmin in (0, 1):
+                C.norm_set_wave_min(wmin)
+                bench_norm(T, H, 0)
+                print(json.dumps({"norm_wave": wmin}), flush=True)
+        C.norm_set_wave_min(0)
     if "lmsample" in which:  # lm_head + sampler, segment maxima on / off
         bench_lmhead_sample(256, 50257, 1600)
         bench_lmhead_sample(256, 50257, 768)
