@@ -476,12 +476,51 @@ class StageWorker(racecheck.Shared):
             # the native path posts every receive in stream order itself: no
             # look-ahead posting of the next step's first receive
             following = []
+        if self._merged_prefill(plan, items):
+            return
         if items:
             self._post(items[0])
         for i, gp in enumerate(items):
             nx = items[i + 1] if i + 1 < len(items) else (following[0] if following else None)
             with self.on_lane(gp.g), trace_range(f"stage{self.r}/step{plan.step}/g{gp.g}"):
                 self._item(plan, gp, nx)
+
+    # One stage: the prefill items of a step in which every group only joins
+    # sequences (a session start) run as ONE forward over all their chunks on
+    # the first item's lane -- GEMMs of every group's rows together instead of
+    # one per group on concurrent lanes; each group's sampled first tokens go
+    # to its own token-return vector and the other lanes wait for the work.
+    MERGE_PREFILL = os.environ.get("LSD_MERGE_PREFILL", "0") == "1"
+
+    def _merged_prefill(self, plan: StepPlan, items: List[GroupPlan]) -> bool:
+        if not (self.MERGE_PREFILL and self.P == 1 and len(items) > 1 and self.device.type == "cuda"):
+            return False
+        if any(gp.kind == "fwd_b" or not gp.chunks or gp.b > 0 or gp.rows is not None or gp.ret > 0
+               for gp in items):
+            return False
+        import types
+
+        g0 = items[0].g
+        merged = types.SimpleNamespace(chunks=[c for gp in items for c in gp.chunks], g=g0)
+        with self.on_lane(g0), trace_range(f"stage{self.r}/step{plan.step}/merged-prefill"), self._gpu():
+            self.stage.backend.lane = self.lane_of(g0)
+            mark = self.stats.mark() if (self.stats is not None and plan.timing) else None
+            ids = self._prefill(merged, self.groups[g0], None)
+            off = 0
+            for gp in items:
+                J = gp.n_final
+                if J:
+                    gs = self.groups[gp.g]
+                    gs.ensure_tokret(self, J)
+                    gs.tokret[:J].copy_(ids[off: off + J])
+                    off += J
+            if mark is not None:
+                self.stats.marks.append((mark, self.stats.mark()))
+            ev = torch.cuda.Event()
+            ev.record()
+        for lane in {self.lane_of(gp.g) for gp in items} - {self.lane_of(g0)}:
+            self.lanes[lane].wait_event(ev)
+        return True
 
     def _new_event(self, timing: bool) -> torch.cuda.Event:
         """A created (recorded once) event whose raw handle C++ can record

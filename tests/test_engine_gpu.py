@@ -171,6 +171,24 @@ def test_prefill_chunk_graphs_bit_identical(monkeypatch, chunk):
     assert sum(w.pf_replays for w in e.workers) > 0
 
 
+def test_merged_prefill_equals_per_group(monkeypatch):
+    """One stage, every group joining at once: the step's prefill items as one
+    forward (pipeline.py _merged_prefill) give the per-group path's greedy
+    tokens.  The merged GEMMs have other row counts (other kernels, other
+    rounding), so this compares greedy decoding of the small test model,
+    whose margins dwarf bf16 rounding; the kernels are deterministic."""
+    from llm_sharding_demo_amd.parallel.pipeline import StageWorker
+
+    sp = SamplingParams(greedy=True, max_new_tokens=6)
+    prompts = [[i + 1, 2 * i + 3, 5, i % 7 + 1] for i in range(12)]
+    monkeypatch.setattr(StageWorker, "MERGE_PREFILL", False)
+    want = _engine("gpt2-test").generate_ids(prompts, sp, microbatches=3)
+    monkeypatch.setattr(StageWorker, "MERGE_PREFILL", True)
+    e = _engine("gpt2-test")
+    for _ in range(2):
+        assert e.generate_ids(prompts, sp, microbatches=3) == want
+
+
 def test_prefill_graphs_bounded(monkeypatch):
     """Serving with changing prompt mixes: at most PREFILL_GRAPHS_MAX prefill
     graphs stay captured per group (oldest dropped), tokens unchanged."""
