@@ -490,7 +490,10 @@ class StageWorker(racecheck.Shared):
     # the first item's lane -- GEMMs of every group's rows together instead of
     # one per group on concurrent lanes; each group's sampled first tokens go
     # to its own token-return vector and the other lanes wait for the work.
-    MERGE_PREFILL = os.environ.get("LSD_MERGE_PREFILL", "0") == "1"
+    # GPT-2 XL headline: prefill 209-210 -> 198 ms (65 K-row GEMMs, MLP-up on
+    # hipBLASLt from 64 K rows), GPT-2 small 21.2 -> 18.8 ms
+    # (profiles/r5_merge_prefill.log); LSD_MERGE_PREFILL=0 keeps one item per group.
+    MERGE_PREFILL = os.environ.get("LSD_MERGE_PREFILL", "1") == "1"
 
     def _merged_prefill(self, plan: StepPlan, items: List[GroupPlan]) -> bool:
         if not (self.MERGE_PREFILL and self.P == 1 and len(items) > 1 and self.device.type == "cuda"):
