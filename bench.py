@@ -274,9 +274,11 @@ def check_against_one_gpu(cfg, eng, prompts, sp, got) -> dict:
     groups = max(1, min(eng.M, want_seqs // rows))
     n = min(groups * rows, len(prompts), len(got))
     t0 = time.perf_counter()
+    # merge_prefill off: the pipeline prefills each group separately, and a
+    # merged prefill's GEMMs (other row counts) would round differently
     ref_cfg = dataclasses.replace(cfg, num_stages=1, dp_replicas=1, max_batch=groups * rows,
                                   num_microbatches=groups, transport="auto",
-                                  device=str(eng.devices[0]))
+                                  device=str(eng.devices[0]), merge_prefill=False)
     ref = Engine(ref_cfg, mode="local")
     try:
         want = ref.generate_ids(prompts[:n], [sp] * n)

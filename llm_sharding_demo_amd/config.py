@@ -259,6 +259,11 @@ class EngineConfig:
     # Prefill tokens per microbatch group per step when requests join a
     # running batch (0 = unlimited: every waiting prompt joins at once).
     prefill_budget: int = 0
+    # One stage: a step's prefill items of groups that all only join
+    # sequences run as one forward (parallel/pipeline.py _merged_prefill).
+    # Off for references that must match a multi-stage pipeline bit for bit
+    # (other GEMM row counts round differently).
+    merge_prefill: bool = True
     # Fraction of the HBM left after the weights that the KV cache may use.
     kv_fraction: float = 0.85
     # Serving: record per-stage busy / bubble timing on one pipeline session

@@ -496,7 +496,8 @@ class StageWorker(racecheck.Shared):
     MERGE_PREFILL = os.environ.get("LSD_MERGE_PREFILL", "1") == "1"
 
     def _merged_prefill(self, plan: StepPlan, items: List[GroupPlan]) -> bool:
-        if not (self.MERGE_PREFILL and self.P == 1 and len(items) > 1 and self.device.type == "cuda"):
+        if not (getattr(self, "merge_prefill", self.MERGE_PREFILL) and self.P == 1 and len(items) > 1
+                and self.device.type == "cuda"):
             return False
         if any(gp.kind == "fwd_b" or not gp.chunks or gp.b > 0 or gp.rows is not None or gp.ret > 0
                for gp in items):

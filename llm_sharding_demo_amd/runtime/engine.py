@@ -342,9 +342,11 @@ class Engine(racecheck.Shared):
     def _worker(self, st: StageModel, t, i: int) -> StageWorker:
         if self.cfg.wire_dtype not in ("fp32", "bf16"):
             raise ValueError(f"wire_dtype must be fp32 or bf16, got {self.cfg.wire_dtype!r}")
-        return StageWorker(st, t, i, self.P, scratch_slot=self.kv_slots,
-                           compat_slot=self.kv_slots + 1,
-                           wire=torch.bfloat16 if self.cfg.wire_dtype == "bf16" else None)
+        w = StageWorker(st, t, i, self.P, scratch_slot=self.kv_slots,
+                        compat_slot=self.kv_slots + 1,
+                        wire=torch.bfloat16 if self.cfg.wire_dtype == "bf16" else None)
+        w.merge_prefill = w.MERGE_PREFILL and self.cfg.merge_prefill
+        return w
 
     @property
     def is_coordinator(self) -> bool:

@@ -131,7 +131,7 @@ def test_devloop_pipeline_bit_identical_and_native(P, chunk):
 
     sp = SamplingParams(temperature=0.8, top_k=20, seed=7, max_new_tokens=12)
     prompts = [[i + 1, 2 * i + 3, 5] for i in range(12)]
-    one = Engine(EngineConfig(model_id="gpt2-test", num_stages=1, max_batch=16, device="cuda",
+    one = Engine(EngineConfig(model_id="gpt2-test", num_stages=1, max_batch=16, device="cuda", merge_prefill=False,
                               num_microbatches=2 * P, prefill_chunk=chunk)).generate_ids(prompts, sp)
     e = _engine(P, chunk)
     assert isinstance(e.workers[1].t, DeviceLoopTransport)

@@ -59,7 +59,7 @@ def test_two_rank_pipeline_matches_single_gpu(tmp_path, dp):
     from llm_sharding_demo_amd.runtime.engine import Engine
 
     one = Engine(EngineConfig(model_id="gpt2-test", num_stages=1, max_batch=8, device="cuda",
-                              max_seq_len=128))
+                              max_seq_len=128, merge_prefill=False))
     ref = one.generate_ids(prompts, SamplingParams(temperature=0.8, top_k=20, seed=5,
                                                    max_new_tokens=10))
     assert dist_out == ref

@@ -104,7 +104,7 @@ def test_graphs_equal_eager_blaslt_silu(monkeypatch):
 def test_pipeline_stages_bit_identical_on_one_gpu():
     prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 50)), [7] * 9]
     sp = SamplingParams(temperature=0.8, top_k=20, seed=5, max_new_tokens=10)
-    one = _engine("gpt2-test").generate_ids(prompts, sp)
+    one = _engine("gpt2-test", merge_prefill=False).generate_ids(prompts, sp)
     two = _engine("gpt2-test", P=2).generate_ids(prompts, sp, microbatches=2)
     four = _engine("gpt2-test", P=4).generate_ids(prompts, sp, microbatches=4)
     assert one == two == four
@@ -221,7 +221,8 @@ def test_loopback_multi_stage_bit_identical(P, chunk):
     # not bit-equal -- tools/check_m1.py)
     # chunked and one-shot prefill round differently (other GEMM row counts
     # and kernels), so the one-stage reference uses the same chunks
-    one = _engine("gpt2-test", num_microbatches=2 * P, prefill_chunk=chunk).generate_ids(prompts, sp)
+    one = _engine("gpt2-test", num_microbatches=2 * P, prefill_chunk=chunk,
+                  merge_prefill=False).generate_ids(prompts, sp)
     e = Engine(EngineConfig(model_id="gpt2-test", num_stages=P, max_batch=16, device="cuda",
                             num_microbatches=2 * P, transport="loopback", prefill_chunk=chunk))
     from llm_sharding_demo_amd.parallel.comm import LoopbackTransport

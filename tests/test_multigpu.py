@@ -117,7 +117,7 @@ def _one_stage(device, dp_groups, greedy=True):
     from llm_sharding_demo_amd.runtime.engine import Engine
 
     eng = Engine(EngineConfig(model_id="gpt2-test", num_stages=1, max_batch=12, device=device,
-                              num_microbatches=dp_groups, max_seq_len=128))
+                              num_microbatches=dp_groups, max_seq_len=128, merge_prefill=False))
     sp = SamplingParams(greedy=greedy, temperature=0.8, top_k=20, seed=5, max_new_tokens=10)
     out = eng.generate_ids(PROMPTS, sp)
     eng.shutdown()
