@@ -380,11 +380,18 @@ class HipBackend(Backend):
         target = self.SK_TARGET or max(128, 384 // max(1, self.concurrency))
         return max(1, min(math.ceil(target / tiles), K // 32 // self.SK_MIN_STEPS or 1))
 
+    # non-residual decode GEMMs with a short K (GPT-2 small, K = 768) run tiled
+    # at any row count above the GEMV: the split-K kernel's last-arriver
+    # combine costs more than the k-loop it splits -- QKV 2304 x 768 at 8-128
+    # rows 9.9-15.7 -> 7.6-8.0 us, MLP-up 3072 x 768 9.5-12.3 -> 7.8-8.3 us
+    # (tools/bench_d256.py, profiles/r5_small_k_routing.log).  0 = off
+    TILED_SHORT_K = int(os.environ.get("LSD_TILED_SHORT_K", "1024"))
+
     def _gemm_kw(self, M: int, N: int, K: int, nw: int = 1):
         bn = self._d256_bn(M, N, K)
         if bn:
             return self._d256_kind(bn), self._d256_splits(N, K, bn, self.D256_TARGET)
-        if self._tiled(M, N):
+        if self._tiled(M, N) or (K <= self.TILED_SHORT_K and M <= self.SK_MAX_M and K % 64 == 0):
             return True, self._ring8_splits(M, N, K)
         return False, self._sk_splits(M, N, K, nw)
 

@@ -104,6 +104,23 @@ def main():
                 kind = 3 if bn == 128 else 2
 
                 def run():
+                    if r8 == "tiled":  # force the tiled (ring) routing, one split
+                        w = ws[it[0] % nw]
+                        it[0] += 1
+                        if resid:
+                            slab = C.linear_residual(a, w, bias, x, 1, True, cnt, False)
+                            return x
+                        return C.linear(a, w, bias, act, True, 1, cnt)
+                    if r8 == "lt":  # hipBLASLt with its own epilogue (bias / GELU / fp32 accumulate)
+                        w = ws[it[0] % nw]
+                        it[0] += 1
+                        if resid:
+                            C.blaslt_residual(a, w, bias, x)
+                            C.norm(x, None, None, bias, None, 0.0, True, None, False)
+                            return x
+                        if f32:
+                            return C.linear_f32(a, w, True, 1, cnt)
+                        return C.blaslt_linear(a, w, bias, act if act in (0, 1) else 0)
                     C.gemm_set_ring8(r8 & 15 if not isinstance(r8, str) else HipBackend.RING8)  # read at launch
                     C.gemm_set_ring8_flags((r8 >> 4) & 15 if not isinstance(r8, str) else 0)
                     w = ws[it[0] % nw]
@@ -135,6 +152,12 @@ def main():
 
             cases = [("ring", 0, 1, int(os.environ.get("D256_BASE_R8", "0")))]
             for v in variants:
+                if v == "tiled":  # the tiled kernels whatever the routing picks
+                    cases.append(("tiled", 0, 1, "tiled"))
+                    continue
+                if v == "lt":  # hipBLASLt (csrc/blaslt.cpp), GELU / bias epilogues
+                    cases.append(("blaslt", 0, 1, "lt"))
+                    continue
                 if v.startswith("knob:"):  # f32 shapes: a launch-routing knob (KNOBS)
                     if f32:
                         cases.append((v[5:], 0, 1, v[5:]))
