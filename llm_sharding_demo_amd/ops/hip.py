@@ -142,13 +142,14 @@ class HipBackend(Backend):
     BLASLT_MIN_M = int(os.environ.get("LSD_BLASLT_MIN_M", "4096"))
     BLASLT_RESID_MIN_K = int(os.environ.get("LSD_BLASLT_RESID_MIN_K", "4096"))
     BLASLT_GELU_MIN_M = int(os.environ.get("LSD_BLASLT_GELU_MIN_M", "65536"))
-    # decode gate_up (SiLU * up) from this many rows: the hipBLASLt GEMM, then
-    # the elementwise pass (elementwise.hip).  Alone, Llama-3 8B at 512 rows
-    # 132 -> 109 + ~8 us (tools/bench_llama_blaslt.py), but the 512-sequence
-    # bench lost 1-1.5 % with it (30.9 / 30.7k vs 31.2 / 31.1k tok/s,
-    # profiles/r5_llama_blaslt.log): off (0) by default, LSD_BLASLT_SILU_MIN_M
-    # turns it on
-    BLASLT_SILU_MIN_M = int(os.environ.get("LSD_BLASLT_SILU_MIN_M", "0"))
+    # decode gate_up (SiLU * up) at BLASLT_SILU_MIN_M..MAX_M rows: the hipBLASLt
+    # GEMM, then the elementwise pass (elementwise.hip).  Llama-3 8B bench
+    # (profiles/r5_llama_blaslt.log): 128 rows +1.7 % (18.15 / 18.12k vs 17.84k
+    # tok/s), 256 rows -1.2 %, 512 rows -1 to -1.5 % although faster alone
+    # there (132 -> 109 + ~8 us, tools/bench_llama_blaslt.py): on for 64-128
+    # rows.  MIN 0 = off
+    BLASLT_SILU_MIN_M = int(os.environ.get("LSD_BLASLT_SILU_MIN_M", "64"))
+    BLASLT_SILU_MAX_M = int(os.environ.get("LSD_BLASLT_SILU_MAX_M", "128"))
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
     # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:
@@ -543,7 +544,7 @@ class HipBackend(Backend):
             y = self.C.blaslt_linear(a, w, b, code, self.lane)
             if y is not None:
                 return y
-        if code == 2 and self.BLASLT_SILU_MIN_M and a.shape[0] >= self.BLASLT_SILU_MIN_M \
+        if code == 2 and self.BLASLT_SILU_MIN_M and self.BLASLT_SILU_MIN_M <= a.shape[0] <= self.BLASLT_SILU_MAX_M \
                 and getattr(self, "decode", False) and a.is_contiguous() and w.shape[0] % 32 == 0:
             y = self.C.blaslt_linear(a, w, b, 0, self.lane)
             if y is not None:

@@ -120,7 +120,9 @@ def main():
                             return x
                         if f32:
                             return C.linear_f32(a, w, True, 1, cnt)
-                        return C.blaslt_linear(a, w, bias, act if act in (0, 1) else 0)
+                        if act == 2:  # SiLU * up: the GEMM, then the elementwise pass
+                            return C.silu_mul(C.blaslt_linear(a, w, bias, 0))
+                        return C.blaslt_linear(a, w, bias, act)
                     C.gemm_set_ring8(r8 & 15 if not isinstance(r8, str) else HipBackend.RING8)  # read at launch
                     C.gemm_set_ring8_flags((r8 >> 4) & 15 if not isinstance(r8, str) else 0)
                     w = ws[it[0] % nw]
