@@ -149,6 +149,8 @@ class HipBackend(Backend):
     # there (132 -> 109 + ~8 us, tools/bench_llama_blaslt.py): on for 64-128
     # rows.  MIN 0 = off
     BLASLT_SILU_MIN_M = int(os.environ.get("LSD_BLASLT_SILU_MIN_M", "64"))
+    # decode MLP-up (bias + GELU) on hipBLASLt from this many rows (0 = off)
+    BLASLT_DECODE_GELU_MIN_M = int(os.environ.get("LSD_BLASLT_DECODE_GELU_MIN_M", "0"))
     BLASLT_SILU_MAX_M = int(os.environ.get("LSD_BLASLT_SILU_MAX_M", "128"))
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
@@ -539,7 +541,9 @@ class HipBackend(Backend):
             return self.C.gemv(x, w, b, code, nc, gw, gb, eps, None, None, None, None, None,
                                0, 0, 0, None)
         a = self.materialize(a)
-        if code == 1 and self._blaslt(a.shape[0]) and a.shape[0] >= self.BLASLT_GELU_MIN_M \
+        dec_gelu = (code == 1 and self.BLASLT_DECODE_GELU_MIN_M and getattr(self, "decode", False)
+                    and a.shape[0] >= self.BLASLT_DECODE_GELU_MIN_M)
+        if ((code == 1 and self._blaslt(a.shape[0]) and a.shape[0] >= self.BLASLT_GELU_MIN_M) or dec_gelu) \
                 and a.is_contiguous():
             y = self.C.blaslt_linear(a, w, b, code, self.lane)
             if y is not None:
