@@ -149,8 +149,12 @@ class HipBackend(Backend):
     # there (132 -> 109 + ~8 us, tools/bench_llama_blaslt.py): on for 64-128
     # rows.  MIN 0 = off
     BLASLT_SILU_MIN_M = int(os.environ.get("LSD_BLASLT_SILU_MIN_M", "64"))
-    # decode MLP-up (bias + GELU) on hipBLASLt from this many rows (0 = off)
-    BLASLT_DECODE_GELU_MIN_M = int(os.environ.get("LSD_BLASLT_DECODE_GELU_MIN_M", "0"))
+    # decode MLP-up (bias + GELU) on hipBLASLt from this many rows: GPT-2 XL at
+    # 384 / 512 rows 24.6 / 25.3 -> 21.3 / 22.6 us alone; 1024 sequences
+    # (2 x 512) 56.2k -> 56.7k tok/s, p50 14.95 -> 14.68 ms
+    # (profiles/r5_xl_decode_gelu.log).  Below 384 rows the ring kernels win
+    # (profiles/r5_small_k_routing.log).  0 = off
+    BLASLT_DECODE_GELU_MIN_M = int(os.environ.get("LSD_BLASLT_DECODE_GELU_MIN_M", "384"))
     BLASLT_SILU_MAX_M = int(os.environ.get("LSD_BLASLT_SILU_MAX_M", "128"))
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
