@@ -63,6 +63,9 @@ int lsd_gemv_ok(int M, int K, int epi, int norm);
 void lsd_gemv_set_nt(int v);
 hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st);
 hipError_t lsd_silu_mul(const lsd_bf16_t* y, long ldy, lsd_bf16_t* out, long ldo, int M, int F, hipStream_t st);
+hipError_t lsd_qkv_post(const float* y, long ldy, const lsd_bf16_t* bias, const int* tslot, const int* tpos,
+                        const float* rope, lsd_bf16_t* q, lsd_bf16_t* kc, lsd_bf16_t* vc, int M, int q_size,
+                        int kv_size, int hd, int n_kv, int max_seq, hipStream_t st);
 hipError_t lsd_sample(const float* logits, long ld, int B, int V, const float* temp,
                       const int* topk, const int* greedy, const long long* seeds,
                       long long* step, int* out, int advance, const int* active, int* pos,
@@ -637,6 +640,45 @@ void sample_launch(const torch::Tensor& logits, int64_t V, const torch::Tensor& 
 
 // out[m, 16 j + i] = silu(y[m, 32 j + i]) * y[m, 32 j + 16 + i]: the SiLU * up
 // pass over a gate/up-interleaved GEMM output (elementwise.hip)
+// QKV epilogue over an fp32 GEMM output y [M, q_size + 2 kv_size] (the
+// hipBLASLt decode path): returns q bf16 [M, q_size]; k, v (RoPE'd) into the
+// caches -- the same contract as linear_qkv.
+torch::Tensor qkv_post(torch::Tensor y, c10::optional<torch::Tensor> bias, torch::Tensor kc, torch::Tensor vc,
+                       torch::Tensor tslot, torch::Tensor tpos, int64_t q_size, int64_t kv_size, int64_t hd,
+                       c10::optional<torch::Tensor> rope) {
+  need(y, torch::kFloat32, "y");
+  const long M = y.size(0), N = y.size(1);
+  TORCH_CHECK(y.dim() == 2 && y.stride(1) == 1 && y.stride(0) % 4 == 0 &&
+              reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0, "qkv_post: y [M, N] with 16-byte rows");
+  TORCH_CHECK(N == q_size + 2 * kv_size && hd % 8 == 0 && q_size % hd == 0 && kv_size % hd == 0,
+              "qkv_post: N must be q_size + 2 kv_size, head dims multiples of 8");
+  const lsd_bf16_t* b = opt_bias(bias, N);
+  need(kc, torch::kBFloat16, "k_cache");
+  need(vc, torch::kBFloat16, "v_cache");
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.sizes() == kc.sizes() && vc.is_contiguous(),
+              "caches must be contiguous [slots, n_kv, max_seq, hd]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(kc.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(vc.data_ptr()) % 16 == 0, "caches must be 16-byte aligned");
+  TORCH_CHECK(kc.size(3) == hd && kc.size(1) * hd == kv_size, "cache shape mismatch");
+  need(tslot, torch::kInt32, "token_slots");
+  need(tpos, torch::kInt32, "token_pos");
+  TORCH_CHECK(tslot.numel() == M && tpos.numel() == M && tslot.is_contiguous() && tpos.is_contiguous(),
+              "token_slots/token_pos must be contiguous [M]");
+  const float* rp = nullptr;
+  if (rope.has_value()) {
+    need(*rope, torch::kFloat32, "rope");
+    TORCH_CHECK(rope->is_contiguous() && rope->dim() == 3 && rope->size(1) == hd / 2 && rope->size(2) == 2 &&
+                rope->size(0) >= kc.size(2), "rope table must be [>=max_seq, hd/2, 2]");
+    rp = rope->data_ptr<float>();
+  }
+  auto q = torch::empty({M, q_size}, y.options().dtype(torch::kBFloat16));
+  check_hip(lsd_qkv_post(y.data_ptr<float>(), y.stride(0), b, tslot.data_ptr<int>(), tpos.data_ptr<int>(), rp,
+                         reinterpret_cast<lsd_bf16_t*>(q.data_ptr()), bptr_mut(kc), bptr_mut(vc), (int)M,
+                         (int)q_size, (int)kv_size, (int)hd, (int)kc.size(1), (int)kc.size(2), cur_stream()),
+            "qkv_post");
+  return q;
+}
+
 torch::Tensor silu_mul(torch::Tensor y) {
   need(y, torch::kBFloat16, "y");
   TORCH_CHECK(y.dim() == 2 && y.stride(1) == 1 && y.size(1) % 32 == 0, "silu_mul: y [M, 2F], 2F % 32 == 0");
@@ -697,6 +739,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pos") = py::none(), py::arg("segmax") = py::none());
   m.def("gemv", &gemv);
   m.def("silu_mul", &silu_mul);
+  m.def("qkv_post", &qkv_post);
   // GEMV weight stream with non-temporal loads (A/B knob, LSD_GEMV_NT)
   m.def("gemv_set_nt", [](int64_t v) { lsd_gemv_set_nt((int)v); });
   m.def("gemv_ok", [](int64_t M, int64_t K, int64_t epi, int64_t norm) {

@@ -8,8 +8,10 @@
 //   * MLP-up: y = gelu_new(a @ w^T + b), bf16 out      (HIPBLASLT_EPILOGUE_GELU_BIAS)
 //   * residual projections: x += a @ w^T + b, fp32 x   (beta = 1 with C = D = x,
 //     HIPBLASLT_EPILOGUE_BIAS; bf16 A / B, fp32 C / D)
-// QKV (its epilogue scatters K / V into the paged cache) and every decode GEMM
-// stay on the hand-written kernels.  Row-major y[M, N] = a[M, K] w[N, K]^T is
+// QKV (its epilogue scatters K / V into the paged cache) stays on the
+// hand-written kernels except Llama-3 8B's 512-row decode QKV, which runs here
+// with fp32 output and a separate RoPE / cache-append pass (blaslt_f32); the
+// other decode GEMMs stay hand-written.  Row-major y[M, N] = a[M, K] w[N, K]^T is
 // the column-major D[N, M] = op_T(W[K, N]) B[K, M]: transa = T, m = N, n = M.
 // The bias runs along D's rows (our columns) as the epilogue expects.
 //
@@ -148,6 +150,20 @@ void lsd_register_blaslt(pybind11::module& m) {
     run(s, p, b, a, w, 0.f, y.data_ptr(), (int)lane);
     return y;
   }, py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("lane") = 0);
+  // y = a @ w^T, fp32 [M, N] (no bias: the caller's pass adds it -- the QKV
+  // epilogue, kernels/elementwise.hip qkv_post); None when no algorithm
+  m.def("blaslt_f32", [](torch::Tensor a, torch::Tensor w, int64_t lane) -> c10::optional<torch::Tensor> {
+    check_operands(a, w);
+    const c10::DeviceGuard guard(a.device());
+    const long M = a.size(0), N = w.size(0), K = a.size(1);
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& s = state(a, (int)lane);
+    auto& p = plan(s, M, N, K, HIPBLASLT_EPILOGUE_DEFAULT, true);
+    if (!p.ok) return c10::nullopt;
+    auto y = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
+    run(s, p, nullptr, a, w, 0.f, y.data_ptr(), (int)lane);
+    return y;
+  }, py::arg("a"), py::arg("w"), py::arg("lane") = 0);
   // x += a @ w^T + bias (x fp32 [M, N], in place); false when the library has
   // no algorithm for the shape (nothing was issued)
   m.def("blaslt_residual", [](torch::Tensor a, torch::Tensor w, c10::optional<torch::Tensor> bias,

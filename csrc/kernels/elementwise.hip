@@ -27,6 +27,58 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(const bf16* __restrict__ 
   st8(out + (long)m * ldo + o, r);
 }
 
+// QKV epilogue over an fp32 GEMM output (hipBLASLt, csrc/blaslt.cpp) -- the
+// same math as gemm.hip EPI_QKV: y = acc + bias; RoPE on adjacent (even, odd)
+// column pairs of q and k (weights pre-permuted, ops/hip.py
+// rope_pair_permutation) with the (cos, sin) of the token's position; q ->
+// out bf16 [M, q_size]; k / v -> the caches at [slot][kv head][pos][d].  One
+// thread per 8 columns: two 16-byte fp32 loads, one 16-byte bf16 store (8
+// columns never straddle a head: hd % 8 == 0).
+__global__ __launch_bounds__(256) void qkv_post_kernel(const float* __restrict__ y, long ldy,
+                                                       const bf16* __restrict__ bias, const int* __restrict__ tslot,
+                                                       const int* __restrict__ tpos, const float* __restrict__ rope,
+                                                       bf16* __restrict__ q, bf16* __restrict__ kc,
+                                                       bf16* __restrict__ vc, int M, int q_size, int kv_size, int hd,
+                                                       int n_kv, int max_seq) {
+  const int N = q_size + 2 * kv_size, per_row = N / 8;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)M * per_row) return;
+  const int m = (int)(idx / per_row);
+  const int n = (int)(idx % per_row) * 8;
+  const f32x4* src = reinterpret_cast<const f32x4*>(y + (long)m * ldy + n);
+  const f32x4 a = src[0], b = src[1];
+  float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  if (bias) {
+    const bf16x8 bb = ld8(bias + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += bf2f(bb[j]);
+  }
+  const int qk = q_size + kv_size;
+  const int pos = tpos[m];
+  if (rope != nullptr && n < qk) {
+    const int d0 = (n < q_size ? n : n - q_size) % hd;
+    const f32x4* cs = reinterpret_cast<const f32x4*>(rope + ((long)pos * (hd >> 1) + (d0 >> 1)) * 2);
+    const f32x4 c0 = cs[0], c1 = cs[1];  // (cos, sin) of pairs d0/2 .. d0/2 + 3
+    const float cc[4] = {c0[0], c0[2], c1[0], c1[2]}, ss[4] = {c0[1], c0[3], c1[1], c1[3]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float e = v[2 * k], o = v[2 * k + 1];
+      v[2 * k] = e * cc[k] - o * ss[k];
+      v[2 * k + 1] = o * cc[k] + e * ss[k];
+    }
+  }
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(v[j]);
+  if (n < q_size) {
+    st8(q + (long)m * q_size + n, r);
+  } else {
+    const int c = n < qk ? n - q_size : n - qk;
+    bf16* cache = n < qk ? kc : vc;
+    st8(cache + (((long)tslot[m] * n_kv + c / hd) * max_seq + pos) * hd + c % hd, r);
+  }
+}
+
 }  // namespace lsd
 
 using namespace lsd;
@@ -37,5 +89,16 @@ extern "C" hipError_t lsd_silu_mul(const bf16* y, long ldy, bf16* out, long ldo,
   if (F % 16 != 0) return hipErrorInvalidValue;
   const long n = (long)M * (F / 8);
   hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, y, ldy, out, ldo, M, F);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t lsd_qkv_post(const float* y, long ldy, const bf16* bias, const int* tslot, const int* tpos,
+                                   const float* rope, bf16* q, bf16* kc, bf16* vc, int M, int q_size, int kv_size,
+                                   int hd, int n_kv, int max_seq, hipStream_t st) {
+  if (M == 0) return hipSuccess;
+  if (hd % 8 != 0 || q_size % hd != 0 || kv_size % hd != 0) return hipErrorInvalidValue;
+  const long n = (long)M * ((q_size + 2 * kv_size) / 8);
+  hipLaunchKernelGGL(qkv_post_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, y, ldy, bias, tslot, tpos,
+                     rope, q, kc, vc, M, q_size, kv_size, hd, n_kv, max_seq);
   return hipGetLastError();
 }

@@ -156,6 +156,12 @@ class HipBackend(Backend):
     # (profiles/r5_small_k_routing.log).  0 = off
     BLASLT_DECODE_GELU_MIN_M = int(os.environ.get("LSD_BLASLT_DECODE_GELU_MIN_M", "384"))
     BLASLT_SILU_MAX_M = int(os.environ.get("LSD_BLASLT_SILU_MAX_M", "128"))
+    # decode QKV from this many rows with K >= BLASLT_QKV_MIN_K on hipBLASLt
+    # (fp32 out) + the RoPE / cache-append pass (elementwise.hip qkv_post):
+    # Llama-3 8B at 512 rows 52.5 us on the 8-wave ring vs 38.6 us for the
+    # library GEMM alone (profiles/r5_llama_blaslt.log).  0 = off
+    BLASLT_QKV_MIN_M = int(os.environ.get("LSD_BLASLT_QKV_MIN_M", "512"))
+    BLASLT_QKV_MIN_K = int(os.environ.get("LSD_BLASLT_QKV_MIN_K", "4096"))
     # Decode GEMM workgroup target (column tiles x K splits).  With c microbatch
     # lanes running concurrently each GEMM should fill ~1/c of the chip so the
     # lanes' kernels co-reside: 384 alone, 192 with two lanes (bench sweep:
@@ -475,6 +481,12 @@ class HipBackend(Backend):
                                meta.token_slots, meta.token_pos, mcfg.q_size, mcfg.kv_size,
                                mcfg.head_dim, self._rope)
         xn = self.materialize(xn)
+        if (self.BLASLT_QKV_MIN_M and getattr(self, "decode", False) and xn.shape[0] >= self.BLASLT_QKV_MIN_M
+                and w.shape[1] >= self.BLASLT_QKV_MIN_K and xn.is_contiguous()):
+            y = self.C.blaslt_f32(xn, w, self.lane)
+            if y is not None:
+                return self.C.qkv_post(y, b, cache_k, cache_v, meta.token_slots, meta.token_pos,
+                                       mcfg.q_size, mcfg.kv_size, mcfg.head_dim, self._rope)
         tiled, splits = self._gemm_kw(xn.shape[0], w.shape[0], w.shape[1])
         return self.C.linear_qkv(xn, w, b, cache_k, cache_v, meta.token_slots, meta.token_pos,
                                  mcfg.q_size, mcfg.kv_size, mcfg.head_dim, self._rope,

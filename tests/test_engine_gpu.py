@@ -101,6 +101,22 @@ def test_graphs_equal_eager_blaslt_silu(monkeypatch):
         assert e.generate_ids(prompts, sp) == a
 
 
+def test_graphs_equal_eager_blaslt_qkv(monkeypatch):
+    """Decode QKV on hipBLASLt + the RoPE / cache-append pass (forced from 1
+    row and any K; the default is 512 rows with K >= 4096) inside captured
+    decode graphs gives the eager tokens."""
+    from llm_sharding_demo_amd.ops.hip import HipBackend
+
+    monkeypatch.setattr(HipBackend, "BLASLT_QKV_MIN_M", 1)
+    monkeypatch.setattr(HipBackend, "BLASLT_QKV_MIN_K", 1)
+    prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 50))]
+    sp = SamplingParams(greedy=True, max_new_tokens=12)
+    a = _engine("llama-test", graphs=False).generate_ids(prompts, sp)
+    e = _engine("llama-test", graphs=True)
+    for _ in range(3):  # eager first use, capture, replay
+        assert e.generate_ids(prompts, sp) == a
+
+
 def test_pipeline_stages_bit_identical_on_one_gpu():
     prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 50)), [7] * 9]
     sp = SamplingParams(temperature=0.8, top_k=20, seed=5, max_new_tokens=10)

@@ -692,6 +692,53 @@ def test_silu_mul_after_blaslt(C, CNT, M):
     close(out, C.linear(a, wi, None, 2, True, 1, CNT), 3e-2)
 
 
+@pytest.mark.parametrize("rope", [False, True])
+def test_qkv_post_after_blaslt(C, CNT, rope):
+    """Decode QKV on hipBLASLt (fp32 out) + the RoPE / cache-append pass
+    (elementwise.hip qkv_post): q and both caches against the fp32 reference
+    and against the fused-epilogue kernel (linear_qkv), padding rows on the
+    scratch slot included."""
+    from llm_sharding_demo_amd.ops.hip import rope_pair_permutation, rope_table
+
+    nh, n_kv, hd, H = 8, 2, 128, 512
+    qs, kvs = nh * hd, n_kv * hd
+    T, slots, S = 96, 5, 200
+    a, w, bias = bf(T, H, seed=113), bf(qs + 2 * kvs, H, scale=0.05, seed=114), bf(qs + 2 * kvs, scale=0.1, seed=115)
+    g = torch.Generator().manual_seed(7)
+    tslot = torch.randint(0, slots, (T,), generator=g).int().to(DEV)
+    tpos = torch.randperm(S, generator=g)[:T].int().to(DEV)  # distinct (slot, pos): no write races
+    y_ref = ref.linear(a, w, bias)
+    q_ref = y_ref[:, :qs].reshape(T, nh, hd)
+    k_ref = y_ref[:, qs:qs + kvs].reshape(T, n_kv, hd)
+    v_ref = y_ref[:, qs + kvs:].reshape(T, n_kv, hd)
+    table = None
+    if rope:
+        q_ref = ref.apply_rope(q_ref, tpos.cpu(), 10000.0)
+        k_ref = ref.apply_rope(k_ref, tpos.cpu(), 10000.0)
+        perm = torch.cat([rope_pair_permutation(nh, hd), rope_pair_permutation(n_kv, hd) + qs,
+                          torch.arange(qs + kvs, qs + 2 * kvs)]).to(DEV)
+        w, bias = w[perm].contiguous(), bias[perm].contiguous()
+        table = rope_table(S, hd, 10000.0, DEV)
+    kc, vc = _cache(slots, n_kv, S, hd)
+    kf, vf = _cache(slots, n_kv, S, hd)
+    y = C.blaslt_f32(a, w)
+    assert y is not None and y.dtype == torch.float32
+    q = C.qkv_post(y, bias, kc, vc, tslot, tpos, qs, kvs, hd, table)
+    qf = C.linear_qkv(a, w, bias, kf, vf, tslot, tpos, qs, kvs, hd, table, True, 1, CNT)
+    close(q, qf, 2e-2)
+    close(kc, kf, 2e-2)
+    close(vc, vf, 2e-2)
+    if rope:  # un-permute the pair-interleaved head dims for the reference
+        inv = torch.argsort(rope_pair_permutation(1, hd)).to(DEV)
+        q = q.reshape(T, nh, hd)[:, :, inv]
+        kc = kc[..., inv]
+    kr, vr = _cache(slots, n_kv, S, hd)
+    ref.kv_append(kr, vr, k_ref, v_ref, tslot, tpos)
+    close(q.reshape(T, nh, hd), q_ref, 3e-2)
+    close(kc, kr, 3e-2)
+    close(vc, vr, 3e-2)
+
+
 def _segmax(logits):
     """What linear_f32 writes beside these logits (padding columns included)."""
     B, Vp = logits.shape
