@@ -240,11 +240,14 @@ class HipBackend(Backend):
     # (p50 8.72 ms: 96 KiB of LDS per workgroup), so 3 slots.
     RING8 = int(os.environ.get("LSD_RING8", "2"))
     RING8_FLAGS = int(os.environ.get("LSD_RING8_FLAGS", "0"))  # A/B bits (gemm.hip)
-    # norms of at least this many rows (prefill) run one wave per row
-    # (norm.hip norm_wave_kernel): 32 K rows x 1600 97.7 -> 53.7 us, x 768
-    # 71.5 -> 24.4 us, x 4096 a tie; GPT-2 XL prefill 217 -> 210 ms
-    # (profiles/r5_normwave.log).  0 = the block-per-row kernel everywhere
-    NORM_WAVE_MIN = int(os.environ.get("LSD_NORM_WAVE_MIN", "4096"))
+    # slab-free norms of at least this many rows run one wave per row
+    # (norm.hip norm_wave_kernel): prefill 32 K rows x 1600 97.7 -> 53.7 us,
+    # x 768 71.5 -> 24.4 us, x 4096 a tie; GPT-2 XL prefill 217 -> 210 ms
+    # (profiles/r5_normwave.log).  Decode: GPT-2 small's ln_1 at 256 rows
+    # (2 x 256 sequences) 351.1-351.3k -> 354.2-355.0k tok/s; 128 rows a tie
+    # (profiles/r5_normwave_decode.log).  Norms that fold split-K slabs keep
+    # the block kernel.  0 = the block-per-row kernel everywhere
+    NORM_WAVE_MIN = int(os.environ.get("LSD_NORM_WAVE_MIN", "256"))
     # lm_head epilogue writes 8-logit segment maxima for the sampler (sample.hip)
     SEGMAX = int(os.environ.get("LSD_SEGMAX", "1"))
     # K splits of the non-residual decode GEMMs on the 8-wave ring (QKV, MLP-up,
