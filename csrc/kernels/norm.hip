@@ -166,27 +166,59 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const void* __restr
   }
 }
 
-// Wave-per-row norm for prefill-sized row counts (no slabs to fold, no row
-// gather): 4 rows per 256-thread block, a row's 16-byte chunks spread over
-// its wave's 64 lanes and all issued before the first use, the statistics
-// merged inside the wave (DPP / permlane butterflies: no LDS, no barrier).
-// Up to 32 rows in flight per CU where the block kernel above holds 8 (2048
-// threads / 256 per row): GPT-2 XL prefill, 32 K rows x 1600, the block
-// kernel streams ~4.5 TB/s (profiles/r4_rejected_norm_loop.log).  A wave per
-// row was slower at decode sizes (profiles/r2_rejected_norm_wave.log), so it
-// only takes T >= lsd_norm_set_wave_min rows.
-template <int MAXC, bool RMS>
-__global__ __launch_bounds__(256) void norm_wave_kernel(const float* __restrict__ x, const bf16* __restrict__ w,
+// Wave-per-row norm: 4 rows per 256-thread block, a row's 16-byte chunks
+// spread over its wave's 64 lanes and all issued before the first use, the
+// statistics merged inside the wave (DPP / permlane butterflies: no LDS, no
+// barrier).  Up to 32 rows in flight per CU where the block kernel above
+// holds 8 (2048 threads / 256 per row): GPT-2 XL prefill, 32 K rows x 1600,
+// the block kernel streams ~4.5 TB/s (profiles/r4_rejected_norm_loop.log).
+// SPL > 0: first fold SPL split-K slabs (bf16 when SB) and the projection
+// bias into the fp32 residual row, written back -- the block kernel's decode
+// job, every slab load of the row issued with the row's.  Taken from
+// lsd_norm_set_wave_min rows (slab-free) / lsd_norm_set_wave_slab_min rows
+// (with slabs).
+template <int MAXC, bool RMS, int SPL = 0, bool SB = false>
+__global__ __launch_bounds__(256) void norm_wave_kernel(float* __restrict__ x, const void* __restrict__ slab_,
+                                                        const bf16* __restrict__ pbias, const bf16* __restrict__ w,
                                                         const bf16* __restrict__ b, bf16* __restrict__ out,
                                                         int T, int H, float eps) {
   const int lane = lane_id();
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= T) return;  // wave-uniform
-  const float* xr = x + (long)row * H;
+  float* xr = x + (long)row * H;
   const int nch = H >> 2;  // 16-byte chunks of the row
   f32x4 v[MAXC];
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) v[i] = *reinterpret_cast<const f32x4*>(xr + 4 * min(lane + i * 64, nch - 1));
+  if constexpr (SPL > 0) {
+    f32x4 part[MAXC][SPL];
+    bf16x4 pb[MAXC];
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      const int c = 4 * min(lane + i * 64, nch - 1);
+#pragma unroll
+      for (int s = 0; s < SPL; ++s) {
+        if constexpr (SB) {
+          const bf16x4 h = __builtin_bit_cast(bf16x4, __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(
+                                                          static_cast<const bf16*>(slab_) + ((long)s * T + row) * H + c)));
+          part[i][s] = f32x4{bf2f(h[0]), bf2f(h[1]), bf2f(h[2]), bf2f(h[3])};
+        } else {
+          part[i][s] = __builtin_nontemporal_load(
+              reinterpret_cast<const f32x4*>(static_cast<const float*>(slab_) + ((long)s * T + row) * H + c));
+        }
+      }
+      if (pbias) pb[i] = ld4(pbias + c);
+    }
+#pragma unroll
+    for (int i = 0; i < MAXC; ++i) {
+      f32x4 a = v[i];
+#pragma unroll
+      for (int s = 0; s < SPL; ++s) a += part[i][s];
+      if (pbias) a += f32x4{bf2f(pb[i][0]), bf2f(pb[i][1]), bf2f(pb[i][2]), bf2f(pb[i][3])};
+      v[i] = a;
+      if (lane + i * 64 < nch) *reinterpret_cast<f32x4*>(xr + 4 * (lane + i * 64)) = a;
+    }
+  }
   bf16x4 wv[MAXC], bv[MAXC];
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) {
@@ -265,18 +297,22 @@ extern "C" hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte,
 
 static int g_norm_wave_min = 0;  // lsd_norm_set_wave_min(): wave-per-row kernel from this many rows (0 = off)
 extern "C" void lsd_norm_set_wave_min(int v) { g_norm_wave_min = v; }
+// the same for norms that fold 1-5 split-K slabs (0 = off: the block kernel)
+static int g_norm_wave_slab_min = 0;
+extern "C" void lsd_norm_set_wave_slab_min(int v) { g_norm_wave_slab_min = v; }
 
 extern "C" hipError_t lsd_norm(float* x, const void* slab, int slab_bf16, int splits, const bf16* pbias,
                                const bf16* w, const bf16* b, bf16* out, int T, int H, float eps,
                                int rms, const int* rows, int nrows, hipStream_t st) {
   const int n = rows ? nrows : T;
   if (n == 0) return hipSuccess;
-  if (g_norm_wave_min > 0 && T >= g_norm_wave_min && !slab && !rows && out && H % 4 == 0 && H <= 4096) {
+  const bool wave_ok = !rows && out && H % 4 == 0 && H <= 4096;
+  if (wave_ok && !slab && g_norm_wave_min > 0 && T >= g_norm_wave_min) {
     const int nch = H / 4;
     const dim3 g((T + 3) / 4), bl(256);
-#define LSD_NORM_W(MC)                                                                         \
-  if (rms) hipLaunchKernelGGL((norm_wave_kernel<MC, true>), g, bl, 0, st, x, w, b, out, T, H, eps); \
-  else hipLaunchKernelGGL((norm_wave_kernel<MC, false>), g, bl, 0, st, x, w, b, out, T, H, eps);
+#define LSD_NORM_W(MC)                                                                                          \
+  if (rms) hipLaunchKernelGGL((norm_wave_kernel<MC, true>), g, bl, 0, st, x, nullptr, nullptr, w, b, out, T, H, eps); \
+  else hipLaunchKernelGGL((norm_wave_kernel<MC, false>), g, bl, 0, st, x, nullptr, nullptr, w, b, out, T, H, eps);
     if (nch <= 256) {
       LSD_NORM_W(4)
     } else if (nch <= 512) {
@@ -285,6 +321,36 @@ extern "C" hipError_t lsd_norm(float* x, const void* slab, int slab_bf16, int sp
       LSD_NORM_W(16)
     }
 #undef LSD_NORM_W
+    return hipGetLastError();
+  }
+  // with slabs: H <= 1024 only -- GPT-2 small (768) mean 353.1k -> 354.7k tok/s
+  // over four pairs, GPT-2 XL (1600, 3 / 5 bf16 slabs, 64 blocks at 256 rows) 50.7-50.9k ->
+  // 49.9-50.1k (profiles/r5_normwave_slab.log)
+  if (wave_ok && slab && splits >= 1 && splits <= 5 && H <= 1024 && g_norm_wave_slab_min > 0 &&
+      T >= g_norm_wave_slab_min) {
+    const int nch = H / 4;
+    const dim3 g((T + 3) / 4), bl(256);
+#define LSD_NORM_WS(MC, S, SB)                                                                                    \
+  if (rms) hipLaunchKernelGGL((norm_wave_kernel<MC, true, S, SB>), g, bl, 0, st, x, slab, pbias, w, b, out, T, H, eps); \
+  else hipLaunchKernelGGL((norm_wave_kernel<MC, false, S, SB>), g, bl, 0, st, x, slab, pbias, w, b, out, T, H, eps);
+#define LSD_NORM_WB(MC, S)     \
+  if (slab_bf16) {             \
+    LSD_NORM_WS(MC, S, true)   \
+  } else {                     \
+    LSD_NORM_WS(MC, S, false)  \
+  }
+#define LSD_NORM_WC(MC)                  \
+  switch (splits) {                      \
+    case 1: LSD_NORM_WB(MC, 1) break;    \
+    case 2: LSD_NORM_WB(MC, 2) break;    \
+    case 3: LSD_NORM_WB(MC, 3) break;    \
+    case 4: LSD_NORM_WB(MC, 4) break;    \
+    default: LSD_NORM_WB(MC, 5) break;   \
+  }
+    LSD_NORM_WC(4)
+#undef LSD_NORM_WC
+#undef LSD_NORM_WB
+#undef LSD_NORM_WS
     return hipGetLastError();
   }
   const int maxv = (H + 1023) / 1024;

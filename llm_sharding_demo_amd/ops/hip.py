@@ -248,6 +248,12 @@ class HipBackend(Backend):
     # (profiles/r5_normwave_decode.log).  Norms that fold split-K slabs keep
     # the block kernel.  0 = the block-per-row kernel everywhere
     NORM_WAVE_MIN = int(os.environ.get("LSD_NORM_WAVE_MIN", "256"))
+    # the same for norms that fold 1-5 split-K slabs, H <= 1024 (GPT-2 small's
+    # ln_2 / ln_f at 256 rows: +0.2-0.8 % over four interleaved pairs, mean
+    # 353.1k -> 354.7k tok/s, p50 1.255 -> 1.248 ms; GPT-2 XL's
+    # H = 1600 lost 1.6 % and stays on the block kernel;
+    # profiles/r5_normwave_slab.log); 0 = off
+    NORM_WAVE_SLAB_MIN = int(os.environ.get("LSD_NORM_WAVE_SLAB_MIN", "256"))
     # lm_head epilogue writes 8-logit segment maxima for the sampler (sample.hip)
     SEGMAX = int(os.environ.get("LSD_SEGMAX", "1"))
     # K splits of the non-residual decode GEMMs on the 8-wave ring (QKV, MLP-up,
@@ -268,6 +274,7 @@ class HipBackend(Backend):
         self.C.gemm_set_ring8(self.RING8)
         self.C.gemm_set_ring8_flags(self.RING8_FLAGS)
         self.C.norm_set_wave_min(self.NORM_WAVE_MIN)
+        self.C.norm_set_wave_slab_min(self.NORM_WAVE_SLAB_MIN)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))

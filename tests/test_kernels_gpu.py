@@ -58,6 +58,37 @@ def test_norm_with_slab_combine(C, H, rms, S, sdt):
     close(y2, y_ref[rows.long()], 2e-2)
 
 
+@pytest.mark.parametrize("H", [768, 1024, 516, 1600])  # 1600: the block kernel (wave path is H <= 1024)
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("S", [1, 3, 5])
+@pytest.mark.parametrize("sdt", [torch.float32, torch.bfloat16])
+def test_norm_wave_with_slabs(C, H, rms, S, sdt):
+    """Decode norms that fold split-K slabs on the wave-per-row kernel
+    (lsd_norm_set_wave_slab_min, forced on from 1 row): the folded residual is
+    bit-equal to the block kernel's (same add order), the normalised output
+    matches the fp32 reference and the block kernel; 258 rows leave a partial
+    last block of 4."""
+    T = 258
+    x0 = torch.randn(T, H, device=DEV)
+    slab = (torch.randn(S, T, H, device=DEV) * 0.1).to(sdt)
+    pb = bf(H, scale=0.1, seed=3)
+    w, b = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16(), bf(H, scale=0.1, seed=4)
+    x_ref = x0 + slab.float().sum(0) + pb.float()
+    y_ref = ref.rmsnorm(x_ref, w, 1e-5) if rms else ref.layernorm(x_ref, w, b, 1e-5)
+    xb = x0.clone()
+    yb = C.norm(xb, slab, pb, w, None if rms else b, 1e-5, rms, None, True)  # block kernel
+    C.norm_set_wave_slab_min(1)
+    try:
+        x = x0.clone()
+        y = C.norm(x, slab, pb, w, None if rms else b, 1e-5, rms, None, True)
+    finally:
+        C.norm_set_wave_slab_min(0)
+    assert torch.equal(x, xb)
+    close(x, x_ref, 1e-5)
+    close(y, y_ref, 2e-2)
+    close(y, yb, 2e-2)
+
+
 @pytest.mark.parametrize("H", [768, 1600, 4096, 1036])
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("T", [5, 4099])
