@@ -174,9 +174,8 @@ __global__ __launch_bounds__(256) void norm_kernel(float* x, const void* __restr
 // the block kernel streams ~4.5 TB/s (profiles/r4_rejected_norm_loop.log).
 // SPL > 0: first fold SPL split-K slabs (bf16 when SB) and the projection
 // bias into the fp32 residual row, written back -- the block kernel's decode
-// job, every slab load of the row issued with the row's.  Taken from
-// lsd_norm_set_wave_min rows (slab-free) / lsd_norm_set_wave_slab_min rows
-// (with slabs).
+// job, every slab load of the row issued with the row's (H <= 1024).  Which
+// row counts take this kernel: lsd_norm below.
 template <int MAXC, bool RMS, int SPL = 0, bool SB = false>
 __global__ __launch_bounds__(256) void norm_wave_kernel(float* __restrict__ x, const void* __restrict__ slab_,
                                                         const bf16* __restrict__ pbias, const bf16* __restrict__ w,
@@ -295,24 +294,69 @@ extern "C" hipError_t lsd_embed(const int* ids, const int* pos, const bf16* wte,
   return hipGetLastError();
 }
 
-static int g_norm_wave_min = 0;  // lsd_norm_set_wave_min(): wave-per-row kernel from this many rows (0 = off)
+// Wave-per-row kernel from g_norm_wave_min rows (any H <= 4096) and from
+// g_norm_wave_narrow_min rows when H <= 1024 (0 = off).  The choice depends on
+// (T, H) only, never on whether slabs are pending: a norm that folds slabs
+// and the same norm after a separate fold (a pipeline stage boundary flushes
+// pending slabs, parallel/pipeline.py) then compute their statistics with the
+// same kernel, so a P-stage pipeline stays bit-identical to one stage.
+static int g_norm_wave_min = 0;
 extern "C" void lsd_norm_set_wave_min(int v) { g_norm_wave_min = v; }
-// the same for norms that fold 1-5 split-K slabs (0 = off: the block kernel)
-static int g_norm_wave_slab_min = 0;
-extern "C" void lsd_norm_set_wave_slab_min(int v) { g_norm_wave_slab_min = v; }
+static int g_norm_wave_narrow_min = 0;
+extern "C" void lsd_norm_set_wave_narrow_min(int v) { g_norm_wave_narrow_min = v; }
+
+static int norm_wave_rows(int H) {
+  int m = g_norm_wave_min;
+  if (H <= 1024 && g_norm_wave_narrow_min > 0 && (m == 0 || g_norm_wave_narrow_min < m)) m = g_norm_wave_narrow_min;
+  return m;
+}
 
 extern "C" hipError_t lsd_norm(float* x, const void* slab, int slab_bf16, int splits, const bf16* pbias,
                                const bf16* w, const bf16* b, bf16* out, int T, int H, float eps,
                                int rms, const int* rows, int nrows, hipStream_t st) {
   const int n = rows ? nrows : T;
   if (n == 0) return hipSuccess;
-  const bool wave_ok = !rows && out && H % 4 == 0 && H <= 4096;
-  if (wave_ok && !slab && g_norm_wave_min > 0 && T >= g_norm_wave_min) {
+  const int wmin = norm_wave_rows(H);
+  const bool wave = !rows && out && H % 4 == 0 && H <= 4096 && wmin > 0 && T >= wmin;
+  const dim3 wg((T + 3) / 4), wb(256);
+  if (wave && slab && H <= 1024 && splits >= 1 && splits <= 8) {
+    // slabs folded in the wave kernel: its row and every slab load in registers
+#define LSD_NORM_WS(S, SB)                                                                                           \
+  if (rms) hipLaunchKernelGGL((norm_wave_kernel<4, true, S, SB>), wg, wb, 0, st, x, slab, pbias, w, b, out, T, H, eps); \
+  else hipLaunchKernelGGL((norm_wave_kernel<4, false, S, SB>), wg, wb, 0, st, x, slab, pbias, w, b, out, T, H, eps);
+#define LSD_NORM_WB(S)     \
+  if (slab_bf16) {         \
+    LSD_NORM_WS(S, true)   \
+  } else {                 \
+    LSD_NORM_WS(S, false)  \
+  }
+    switch (splits) {
+      case 1: LSD_NORM_WB(1) break;
+      case 2: LSD_NORM_WB(2) break;
+      case 3: LSD_NORM_WB(3) break;
+      case 4: LSD_NORM_WB(4) break;
+      case 5: LSD_NORM_WB(5) break;
+      case 6: LSD_NORM_WB(6) break;
+      case 7: LSD_NORM_WB(7) break;
+      default: LSD_NORM_WB(8) break;
+    }
+#undef LSD_NORM_WB
+#undef LSD_NORM_WS
+    return hipGetLastError();
+  }
+  if (wave && slab) {
+    // other slab counts / widths: fold first (the block kernel's combine-only
+    // pass, the same add order), then the slab-free wave kernel below
+    const hipError_t e = lsd_norm(x, slab, slab_bf16, splits, pbias, nullptr, nullptr, nullptr, T, H, eps, rms,
+                                  nullptr, 0, st);
+    if (e != hipSuccess) return e;
+    slab = nullptr;
+  }
+  if (wave) {
     const int nch = H / 4;
-    const dim3 g((T + 3) / 4), bl(256);
-#define LSD_NORM_W(MC)                                                                                          \
-  if (rms) hipLaunchKernelGGL((norm_wave_kernel<MC, true>), g, bl, 0, st, x, nullptr, nullptr, w, b, out, T, H, eps); \
-  else hipLaunchKernelGGL((norm_wave_kernel<MC, false>), g, bl, 0, st, x, nullptr, nullptr, w, b, out, T, H, eps);
+#define LSD_NORM_W(MC)                                                                                           \
+  if (rms) hipLaunchKernelGGL((norm_wave_kernel<MC, true>), wg, wb, 0, st, x, nullptr, nullptr, w, b, out, T, H, eps); \
+  else hipLaunchKernelGGL((norm_wave_kernel<MC, false>), wg, wb, 0, st, x, nullptr, nullptr, w, b, out, T, H, eps);
     if (nch <= 256) {
       LSD_NORM_W(4)
     } else if (nch <= 512) {
@@ -321,36 +365,6 @@ extern "C" hipError_t lsd_norm(float* x, const void* slab, int slab_bf16, int sp
       LSD_NORM_W(16)
     }
 #undef LSD_NORM_W
-    return hipGetLastError();
-  }
-  // with slabs: H <= 1024 only -- GPT-2 small (768) mean 353.1k -> 354.7k tok/s
-  // over four pairs, GPT-2 XL (1600, 3 / 5 bf16 slabs, 64 blocks at 256 rows) 50.7-50.9k ->
-  // 49.9-50.1k (profiles/r5_normwave_slab.log)
-  if (wave_ok && slab && splits >= 1 && splits <= 5 && H <= 1024 && g_norm_wave_slab_min > 0 &&
-      T >= g_norm_wave_slab_min) {
-    const int nch = H / 4;
-    const dim3 g((T + 3) / 4), bl(256);
-#define LSD_NORM_WS(MC, S, SB)                                                                                    \
-  if (rms) hipLaunchKernelGGL((norm_wave_kernel<MC, true, S, SB>), g, bl, 0, st, x, slab, pbias, w, b, out, T, H, eps); \
-  else hipLaunchKernelGGL((norm_wave_kernel<MC, false, S, SB>), g, bl, 0, st, x, slab, pbias, w, b, out, T, H, eps);
-#define LSD_NORM_WB(MC, S)     \
-  if (slab_bf16) {             \
-    LSD_NORM_WS(MC, S, true)   \
-  } else {                     \
-    LSD_NORM_WS(MC, S, false)  \
-  }
-#define LSD_NORM_WC(MC)                  \
-  switch (splits) {                      \
-    case 1: LSD_NORM_WB(MC, 1) break;    \
-    case 2: LSD_NORM_WB(MC, 2) break;    \
-    case 3: LSD_NORM_WB(MC, 3) break;    \
-    case 4: LSD_NORM_WB(MC, 4) break;    \
-    default: LSD_NORM_WB(MC, 5) break;   \
-  }
-    LSD_NORM_WC(4)
-#undef LSD_NORM_WC
-#undef LSD_NORM_WB
-#undef LSD_NORM_WS
     return hipGetLastError();
   }
   const int maxv = (H + 1023) / 1024;

@@ -240,20 +240,19 @@ class HipBackend(Backend):
     # (p50 8.72 ms: 96 KiB of LDS per workgroup), so 3 slots.
     RING8 = int(os.environ.get("LSD_RING8", "2"))
     RING8_FLAGS = int(os.environ.get("LSD_RING8_FLAGS", "0"))  # A/B bits (gemm.hip)
-    # slab-free norms of at least this many rows run one wave per row
-    # (norm.hip norm_wave_kernel): prefill 32 K rows x 1600 97.7 -> 53.7 us,
-    # x 768 71.5 -> 24.4 us, x 4096 a tie; GPT-2 XL prefill 217 -> 210 ms
-    # (profiles/r5_normwave.log).  Decode: GPT-2 small's ln_1 at 256 rows
-    # (2 x 256 sequences) 351.1-351.3k -> 354.2-355.0k tok/s; 128 rows a tie
-    # (profiles/r5_normwave_decode.log).  Norms that fold split-K slabs keep
-    # the block kernel.  0 = the block-per-row kernel everywhere
-    NORM_WAVE_MIN = int(os.environ.get("LSD_NORM_WAVE_MIN", "256"))
-    # the same for norms that fold 1-5 split-K slabs, H <= 1024 (GPT-2 small's
-    # ln_2 / ln_f at 256 rows: +0.2-0.8 % over four interleaved pairs, mean
-    # 353.1k -> 354.7k tok/s, p50 1.255 -> 1.248 ms; GPT-2 XL's
-    # H = 1600 lost 1.6 % and stays on the block kernel;
-    # profiles/r5_normwave_slab.log); 0 = off
-    NORM_WAVE_SLAB_MIN = int(os.environ.get("LSD_NORM_WAVE_SLAB_MIN", "256"))
+    # norms of at least this many rows run one wave per row (norm.hip
+    # norm_wave_kernel): prefill 32 K rows x 1600 97.7 -> 53.7 us, x 768 71.5
+    # -> 24.4 us, x 4096 a tie; GPT-2 XL prefill 217 -> 210 ms
+    # (profiles/r5_normwave.log).  0 = the block-per-row kernel everywhere
+    NORM_WAVE_MIN = int(os.environ.get("LSD_NORM_WAVE_MIN", "4096"))
+    # ... and from this many rows when H <= 1024, with or without split-K
+    # slabs to fold: GPT-2 small decode at 2 x 256 rows 351.1-351.3k ->
+    # 354.2-355.0k tok/s (profiles/r5_normwave_decode.log).  GPT-2 XL's H =
+    # 1600 decode norms lost 1.6 % on it and keep the block kernel
+    # (profiles/r5_normwave_slab.log).  The choice depends on (rows, H) only,
+    # so a pipeline stage boundary (slabs folded before the norm) computes the
+    # same statistics as one stage; 0 = off
+    NORM_WAVE_NARROW_MIN = int(os.environ.get("LSD_NORM_WAVE_NARROW_MIN", "256"))
     # lm_head epilogue writes 8-logit segment maxima for the sampler (sample.hip)
     SEGMAX = int(os.environ.get("LSD_SEGMAX", "1"))
     # K splits of the non-residual decode GEMMs on the 8-wave ring (QKV, MLP-up,
@@ -274,7 +273,7 @@ class HipBackend(Backend):
         self.C.gemm_set_ring8(self.RING8)
         self.C.gemm_set_ring8_flags(self.RING8_FLAGS)
         self.C.norm_set_wave_min(self.NORM_WAVE_MIN)
-        self.C.norm_set_wave_slab_min(self.NORM_WAVE_SLAB_MIN)
+        self.C.norm_set_wave_narrow_min(self.NORM_WAVE_NARROW_MIN)
         self.C.attn_set_max_wg(int(os.environ.get("LSD_ATTN_MAX_WG", "0")))
         self.C.gemv_set_nt(int(os.environ.get("LSD_GEMV_NT", "0")))
         self.C.attn_set_small_waves(int(os.environ.get("LSD_ATTN_SMALL_WAVES", "8")))

@@ -58,14 +58,14 @@ def test_norm_with_slab_combine(C, H, rms, S, sdt):
     close(y2, y_ref[rows.long()], 2e-2)
 
 
-@pytest.mark.parametrize("H", [768, 1024, 516, 1600])  # 1600: the block kernel (wave path is H <= 1024)
+@pytest.mark.parametrize("H", [768, 1024, 516, 1600])  # 1600: the block kernel (narrow threshold: H <= 1024)
 @pytest.mark.parametrize("rms", [False, True])
-@pytest.mark.parametrize("S", [1, 3, 5])
+@pytest.mark.parametrize("S", [1, 3, 6, 8, 12])  # 12: folded by the block kernel first, then the wave kernel
 @pytest.mark.parametrize("sdt", [torch.float32, torch.bfloat16])
 def test_norm_wave_with_slabs(C, H, rms, S, sdt):
-    """Decode norms that fold split-K slabs on the wave-per-row kernel
-    (lsd_norm_set_wave_slab_min, forced on from 1 row): the folded residual is
-    bit-equal to the block kernel's (same add order), the normalised output
+    """Norms that fold split-K slabs on the wave-per-row kernel (H <= 1024 from
+    lsd_norm_set_wave_narrow_min rows, forced from 1 row here): the folded
+    residual is bit-equal to the block kernel's (same add order), the output
     matches the fp32 reference and the block kernel; 258 rows leave a partial
     last block of 4."""
     T = 258
@@ -75,18 +75,48 @@ def test_norm_wave_with_slabs(C, H, rms, S, sdt):
     w, b = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16(), bf(H, scale=0.1, seed=4)
     x_ref = x0 + slab.float().sum(0) + pb.float()
     y_ref = ref.rmsnorm(x_ref, w, 1e-5) if rms else ref.layernorm(x_ref, w, b, 1e-5)
+    C.norm_set_wave_min(0)
+    C.norm_set_wave_narrow_min(0)
     xb = x0.clone()
     yb = C.norm(xb, slab, pb, w, None if rms else b, 1e-5, rms, None, True)  # block kernel
-    C.norm_set_wave_slab_min(1)
+    C.norm_set_wave_narrow_min(1)
     try:
         x = x0.clone()
         y = C.norm(x, slab, pb, w, None if rms else b, 1e-5, rms, None, True)
     finally:
-        C.norm_set_wave_slab_min(0)
+        _norm_defaults(C)
     assert torch.equal(x, xb)
     close(x, x_ref, 1e-5)
     close(y, y_ref, 2e-2)
     close(y, yb, 2e-2)
+
+
+def _norm_defaults(C):
+    from llm_sharding_demo_amd.ops.hip import HipBackend
+
+    C.norm_set_wave_min(HipBackend.NORM_WAVE_MIN)
+    C.norm_set_wave_narrow_min(HipBackend.NORM_WAVE_NARROW_MIN)
+
+
+@pytest.mark.parametrize("T,H", [(258, 768), (258, 1600), (4099, 768), (4099, 1600), (100, 768)])
+@pytest.mark.parametrize("S", [3, 6, 12])
+def test_norm_slab_fold_equals_flush_then_norm(C, T, H, S):
+    """The engine's kernel choice for a norm depends on (rows, H) only: a norm
+    that folds pending slabs and the same norm after a separate fold (what a
+    pipeline stage boundary does) give bit-identical residuals and outputs at
+    the default thresholds -- the property that keeps a P-stage pipeline
+    equal to one stage."""
+    _norm_defaults(C)
+    x0 = torch.randn(T, H, device=DEV)
+    slab = (torch.randn(S, T, H, device=DEV) * 0.1).bfloat16()
+    pb = bf(H, scale=0.1, seed=3)
+    w, b = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16(), bf(H, scale=0.1, seed=4)
+    x1, x2 = x0.clone(), x0.clone()
+    y1 = C.norm(x1, slab, pb, w, b, 1e-5, False, None, True)
+    C.norm(x2, slab, pb, None, None, 0.0, True, None, False)  # fold only (stage-boundary flush)
+    y2 = C.norm(x2, None, None, w, b, 1e-5, False, None, True)
+    assert torch.equal(x1, x2)
+    assert torch.equal(y1, y2)
 
 
 @pytest.mark.parametrize("H", [768, 1600, 4096, 1036])
@@ -107,7 +137,7 @@ def test_norm_wave_per_row(C, H, rms, T):
         close(y, y_ref, 2e-2)
         assert torch.equal(x, x0)
     finally:
-        C.norm_set_wave_min(0)
+        _norm_defaults(C)
 
 
 @pytest.fixture(scope="module")
