@@ -118,8 +118,8 @@ def main():
                             C.blaslt_residual(a, w, bias, x)
                             C.norm(x, None, None, bias, None, 0.0, True, None, False)
                             return x
-                        if f32:
-                            return C.linear_f32(a, w, True, 1, cnt)
+                        if f32:  # fp32 output, no epilogue (csrc/blaslt.cpp blaslt_f32)
+                            return C.blaslt_f32(a, w)
                         if act == 2:  # SiLU * up: the GEMM, then the elementwise pass
                             return C.silu_mul(C.blaslt_linear(a, w, bias, 0))
                         return C.blaslt_linear(a, w, bias, act)
