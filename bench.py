@@ -48,10 +48,13 @@ def parse():
                         "else 1 (weights read once per step)")
     p.add_argument("--dp", type=int, default=int(os.environ.get("BENCH_DP", "1")),
                    help="pipeline replicas: N GPUs = (N/dp)-stage pipeline x dp (default 1: ppN)")
-    p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "nccl"),
-                   help="nccl (RCCL via torch.distributed) | rccl (native RCCL communicator, csrc/comm.cpp) | "
+    p.add_argument("--transport", default=os.environ.get("BENCH_TRANSPORT", "auto"),
+                   help="auto (default: on GPUs the native RCCL communicators with graph-captured edges, "
+                        "self-tested at startup, falling back in process to torch's RCCL groups; ranks "
+                        "sharing one GPU: devloop, then gloo) | rccl | nccl (RCCL via torch.distributed) | "
                         "gloo (host-staged, for rehearsals) | devloop (every rank on ONE GPU: device loopback "
-                        "channels between the rank processes, the rccl code path's rehearsal)")
+                        "channels between the rank processes, the rccl code path's rehearsal) | a,b (an "
+                        "explicit chain: a, falling back to b)")
     p.add_argument("--loopback-stages", type=int, default=0,
                    help="rehearsal: run this many pipeline stages as threads on ONE GPU; "
                         "--batch is then the total batch")
@@ -194,7 +197,9 @@ def main() -> int:
         p50 = statistics.median(step_ms) if step_ms else None
         base = REFERENCE_TOK_S.get(args.model)
         out = {
-            "metric": "output tokens/sec + p50 per-token latency, GPT-2 pipeline at N MI355X",
+            "metric": "output tokens/sec + p50 per-token latency, "
+                      + ("GPT-2" if args.model.startswith(("gpt2", "tiny-gpt2")) else args.model)
+                      + " pipeline at N MI355X",
             "value": round(value, 2), "unit": "tokens/s", "n_gpus": N, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak",
@@ -213,7 +218,7 @@ def main() -> int:
                        "prefill_chunk": chunk,
                        "parallelism": f"pp{P}" + (f"xdp{R}" if R > 1 else "")
                        + ("-loopback-1gpu" if args.loopback_stages else "")
-                       + ("-ranks-on-1gpu" if transport == "devloop" and N > 1 else ""),
+                       + ("-ranks-on-1gpu" if eng.transport_kind == "devloop" and N > 1 else ""),
                        "sampler": "greedy" if args.greedy else "T0.6/top-k40",
                        "hipgraphs": not args.no_graphs},
         }
@@ -224,8 +229,12 @@ def main() -> int:
             out["split_k_slabs"] = "bf16" if C.gemm_slab_bf16() else "fp32"
         if (args.loopback_stages or N > 1) and eng.last_session is not None:
             out["stage_busy"] = [st["busy_fraction"] for st in eng.last_session.stages]
-        if N > 1 or args.loopback_stages:
+        if args.loopback_stages:
             out["transport"] = transport
+        if N > 1:
+            # the data plane that ran, and why the preferred one was left (or null)
+            out["transport"] = eng.transport_kind
+            out["transport_fallback"] = eng.transport_fallback
         if ranks is not None:
             out["pg_world_size"] = ranks[0]["pg_world"]
             out["data_plane_comms"] = sum(r["comms"] for r in ranks)

@@ -193,6 +193,17 @@ class _DistTransport(Transport):
     def barrier(self) -> None:
         self.dist.barrier(group=self.ctrl)
 
+    def agree(self, err: Optional[str], what: str) -> None:
+        """Every rank learns every rank's outcome of one bring-up step; any
+        failure raises the SAME TransportError on all of them, so they leave
+        together (to a fallback transport) instead of one rank waiting in a
+        communicator init or a transfer on a peer that already left."""
+        errs = [None] * self.gworld
+        self.dist.all_gather_object(errs, err, group=self.ctrl)
+        bad = [e for e in errs if e]
+        if bad:
+            raise TransportError(f"{what}: " + "; ".join(bad[:4]) + (" ..." if len(bad) > 4 else ""))
+
     def warmup(self, device) -> None:
         """Eagerly create every edge communicator in a fixed global order so no
         rank blocks in a lazy ncclCommInitRank while its peer waits elsewhere.
@@ -307,7 +318,11 @@ class RcclTransport(_DistTransport):
     Bring-up: the unique id of each communicator is made by its first member
     and broadcast over the gloo control group; members join in a fixed global
     order (edge-major, then lane), so the blocking inits complete left to
-    right, as in `warmup`."""
+    right, as in `warmup`.  Every step is bounded and agreed (`agree`): a
+    failed or hung init on any rank raises the same TransportError on every
+    rank (the engine then falls back to torch's RCCL groups, see
+    `open_data_plane`); an init still blocked at its deadline is left on a
+    daemon thread."""
 
     EDGE_GROUPS = False
     GRAPH_IO = True  # the pipeline may capture send / recv into decode graphs
@@ -316,11 +331,8 @@ class RcclTransport(_DistTransport):
         return "gloo"  # control plane only; the data plane is native
 
     def __init__(self, num_stages: int, replicas: int = 1, lanes: int = 2,
-                 timeout_s: Optional[float] = None):
+                 timeout_s: Optional[float] = None, init_s: float = 120.0):
         super().__init__(num_stages, replicas, timeout_s)
-        from ..ops.hip import _load
-
-        self.C = _load()
         self.L = max(1, lanes)
         self.comms: Dict[tuple, tuple] = {}  # (edge group name, lane) -> (handle, my index)
         self.aborted = False
@@ -332,14 +344,36 @@ class RcclTransport(_DistTransport):
         # keep the abort that would unstick it from running)
         self._issue = threading.Condition()
         self._inflight = 0
-        for name in self.groups:
-            members = self._members(name)
-            for lane in range(self.L):
-                uid = self.C.rccl_unique_id() if self.grank == members[0] else None
-                uid = self.broadcast_object(uid, src=members[0])
-                if self.grank in members:
-                    me = members.index(self.grank)
-                    self.comms[(name, lane)] = (self.C.rccl_comm_init(2, me, uid), me)
+        err = None
+        try:
+            from ..ops.hip import _load
+
+            self.C = _load()
+            self.C.rccl_version()  # resolves librccl and its symbols
+        except Exception as e:  # noqa: BLE001 - every rank must learn the outcome
+            err = f"rank {self.grank}: {type(e).__name__}: {e}"
+        self.agree(err, "native RCCL unavailable")
+        try:
+            for name in self.groups:
+                members = self._members(name)
+                for lane in range(self.L):
+                    uid, err = None, None
+                    if self.grank == members[0]:
+                        try:
+                            uid = self.C.rccl_unique_id()
+                        except Exception as e:  # noqa: BLE001
+                            err = f"rank {self.grank}: ncclGetUniqueId: {e}"
+                    uid = self.broadcast_object(uid, src=members[0])
+                    if self.grank in members and err is None and uid is not None:
+                        me = members.index(self.grank)
+                        h, err = _bounded(lambda: self.C.rccl_comm_init(2, me, uid), init_s,
+                                          f"rank {self.grank}: ncclCommInitRank {name}/lane{lane}")
+                        if h:
+                            self.comms[(name, lane)] = (h, me)
+                    self.agree(err, f"RCCL communicator {name}/lane{lane}")
+        except TransportError:
+            self.abort(drain_s=0.0)  # free the communicators made so far
+            raise
 
     @property
     def num_comms(self) -> int:
@@ -1247,31 +1281,228 @@ def init_distributed(backend: str, device_type: str, timeout_s: float = 600.0) -
 
 
 def make_dist_transport(num_stages: int, kind: str, device, replicas: int = 1,
-                        timeout_s: Optional[float] = None, loop_ring_bytes: int = 256 << 20) -> Transport:
+                        timeout_s: Optional[float] = None, loop_ring_bytes: int = 256 << 20,
+                        warmup: bool = True) -> Transport:
     """`loop_ring_bytes`: devloop channel rings, sized by the engine for the
-    largest message an edge carries (LSD_LOOP_RING_MB overrides)."""
+    largest message an edge carries (LSD_LOOP_RING_MB overrides).
+    `warmup=False`: no unagreed per-rank exchange (`open_data_plane` runs the
+    agreed self-test instead)."""
+    import os
+
     if kind == "rccl":  # native communicator (csrc/comm.cpp), one per (edge, lane)
-        import os
-
         t = RcclTransport(num_stages, replicas, lanes=int(os.environ.get("LSD_LANES", "2")),
-                          timeout_s=timeout_s)
-        t.warmup(device)
-        return t
-    if kind == "nccl":
+                          timeout_s=timeout_s, init_s=float(os.environ.get("LSD_RCCL_INIT_S", "120")))
+    elif kind == "nccl":
         t = NcclTransport(num_stages, replicas, timeout_s)
-        t.warmup(device)
-        return t
-    if kind == "devloop":  # every rank on one GPU: the 1-GPU rehearsal of "rccl"
-        import os
-
+    elif kind == "devloop":  # every rank on one GPU: the 1-GPU rehearsal of "rccl"
         t = IpcLoopTransport(num_stages, replicas, lanes=int(os.environ.get("LSD_LANES", "2")),
                              timeout_s=timeout_s,
                              ring_bytes=int(os.environ.get("LSD_LOOP_RING_MB", "0")) << 20 or loop_ring_bytes,
                              spin_limit_s=float(os.environ.get("LSD_LOOP_SPIN_S", "30")))
+    elif kind == "gloo":
+        t = GlooTransport(num_stages, replicas, timeout_s)  # host-staged, same edge-by-edge bring-up
+    else:
+        raise ValueError(f"unknown transport {kind!r}")
+    if warmup or kind == "nccl":
+        # torch's groups create their p2p communicators lazily: the warmup's
+        # ordered exchange is what creates them without a cross-edge deadlock
         t.warmup(device)
-        return t
-    if kind == "gloo":
-        t = GlooTransport(num_stages, replicas, timeout_s)
-        t.warmup(device)  # same edge-by-edge bring-up as RCCL (host tensors)
-        return t
-    raise ValueError(f"unknown transport {kind!r}")
+    return t
+
+
+# ---------------------------------------------------------------------------
+# Data-plane selection: self-test + agreed in-process fallback
+# ---------------------------------------------------------------------------
+
+def transport_chain(spec: str, device_type: str, shared_gpu: bool = False) -> List[str]:
+    """Data planes to try, in order.  "auto": on GPUs the native RCCL
+    communicators with graph-captured edges (the path the one-GPU devloop
+    rehearsal exercises: `exec_items`, captured send / recv), falling back to
+    torch's RCCL process groups (eager p2p from the Python item loop); rank
+    processes sharing ONE GPU (RCCL refuses two ranks on a device) use the
+    device loopback channels, falling back to host-staged gloo; on CPU gloo.
+    An explicit "a,b" lists the chain itself."""
+    if spec in ("", "auto", "local"):
+        if device_type != "cuda":
+            return ["gloo"]
+        return ["devloop", "gloo"] if shared_gpu else ["rccl", "nccl"]
+    return [k.strip() for k in spec.split(",") if k.strip()]
+
+
+def _bounded(fn, timeout_s: float, what: str):
+    """(result, None) of fn() run on a daemon thread, or (None, error) when
+    it raised or had not returned after `timeout_s` (a blocking communicator
+    init whose peer never arrives: the thread is left behind, the caller
+    moves on)."""
+    box: list = []
+
+    def run():
+        try:
+            box.append((fn(), None))
+        except Exception as e:  # noqa: BLE001
+            box.append((None, f"{what}: {type(e).__name__}: {e}"))
+
+    th = threading.Thread(target=run, daemon=True, name="lsd-bounded")
+    th.start()
+    th.join(timeout_s)
+    if not box:
+        return None, f"{what}: no result after {timeout_s:.0f} s"
+    return box[0]
+
+
+def _drained(device, deadline: float) -> bool:
+    """Wait (bounded) for the work enqueued so far on the current stream."""
+    if device.type != "cuda":
+        return True
+    ev = torch.cuda.Event()
+    ev.record()
+    while not ev.query():
+        if time.monotonic() > deadline:
+            return False
+        time.sleep(200e-6)
+    return True
+
+
+def _pattern(n: int, tag: float, device) -> torch.Tensor:
+    return torch.arange(n, dtype=torch.float32, device=device).mul_(1e-3).add_(tag)
+
+
+def _edge_list(t) -> List[tuple]:
+    """This replica's edges in the global bring-up order: fwd 0..P-2, ret."""
+    P = t.P
+    out = [("fwd", i, i + 1) for i in range(P - 1)]
+    if P > 1:
+        out.append(("ret", P - 1, 0))
+    return out
+
+
+def _captured_exchange(t, device, kind, src, dst, lane, tag, deadline) -> Optional[str]:
+    """One send / receive captured into a hipGraph on each end, replayed
+    twice with fresh data: the decode graphs' edge I/O in miniature."""
+    from .pipeline import GPU_GATE
+
+    n = 4096
+    buf = torch.zeros(n, dtype=torch.float32, device=device)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    begin = getattr(t, "begin_capture", None)
+    io = (0, [])
+    with GPU_GATE.exclusive(), torch.cuda.stream(s):
+        if begin is not None:
+            begin()
+        g.capture_begin(capture_error_mode="thread_local")
+        try:
+            if t.rank == src:
+                t.capture_send(buf, dst, kind, lane)
+            else:
+                t.capture_recv(buf, src, kind, lane)
+        finally:
+            g.capture_end()
+            if begin is not None:
+                io = t.end_capture()
+    torch.cuda.current_stream(device).wait_stream(s)
+    for k in (1, 2):
+        want = _pattern(n, tag + 100.0 * k, device)
+        if t.rank == src:
+            buf.copy_(want)
+        if io[0]:
+            t.replay(g, io[0], io[1])
+        else:
+            with t.issuing():
+                g.replay()
+        if not _drained(device, deadline):
+            return f"captured {kind} {src}->{dst} lane {lane}, replay {k}: not complete by the deadline"
+        if t.rank == dst and not torch.equal(buf, want):
+            return f"captured {kind} {src}->{dst} lane {lane}, replay {k}: wrong data"
+    return None
+
+
+def selftest_data_plane(t: "_DistTransport", device, deadline_s: float = 60.0) -> Optional[str]:
+    """This rank's part of the data-plane self-test, bounded by `deadline_s`:
+    on every (edge, lane) it belongs to, in the global order, one eager
+    exchange of a small and of a 1 MiB message and -- on transports whose
+    decode graphs carry their own transfers -- one exchange captured in a
+    hipGraph on both ends and replayed twice; the receiver checks every byte.
+    Returns None or this rank's error (the caller agrees on the outcome)."""
+    deadline = time.monotonic() + deadline_s
+    capture = device.type == "cuda" and getattr(t, "GRAPH_IO", False)
+    lanes = getattr(t, "L", 1)
+    try:
+        for ei, (kind, src, dst) in enumerate(_edge_list(t)):
+            if t.rank not in (src, dst):
+                continue
+            for lane in range(lanes):
+                tag = 1000.0 * (ei + 1) + 10.0 * lane
+                for n in (1024, 1 << 18):
+                    x = _pattern(n, tag, device)
+                    if t.rank == src:
+                        t.send(x, dst, kind, lane).wait()
+                    else:
+                        got = torch.zeros_like(x)
+                        t.irecv(got, src, kind, lane).wait()
+                    if not _drained(device, deadline):
+                        return (f"rank {t.grank}: eager {kind} {src}->{dst} lane {lane} ({4 * n} B) "
+                                f"not complete after {deadline_s:.0f} s")
+                    if t.rank == dst and not torch.equal(got, x):
+                        return f"rank {t.grank}: eager {kind} {src}->{dst} lane {lane} ({4 * n} B): wrong data"
+                if capture:
+                    err = _captured_exchange(t, device, kind, src, dst, lane, tag, deadline)
+                    if err:
+                        return f"rank {t.grank}: {err}"
+    except Exception as e:  # noqa: BLE001
+        return f"rank {t.grank}: {type(e).__name__}: {e}"
+    return None
+
+
+def _teardown_failed(t, device, drain_s: float = 30.0) -> None:
+    """After a failed self-test: abort the data plane (kernels waiting on a
+    peer return) and let this rank's stream drain before the next transport
+    is brought up."""
+    try:
+        t.abort()
+    except Exception:  # noqa: BLE001
+        pass
+    if not _drained(device, time.monotonic() + drain_s):
+        raise TransportError("a failed data plane did not drain after its abort; cannot fall back")
+
+
+def open_data_plane(chain: List[str], num_stages: int, device, replicas: int = 1,
+                    timeout_s: Optional[float] = None, loop_ring_bytes: int = 256 << 20):
+    """Bring up the first transport of `chain` that passes the self-test on
+    EVERY rank: (transport, kind, fallback reason or None).  Each candidate's
+    bring-up and self-test outcome is agreed over the gloo control group, so
+    all ranks fall back together, in process (no re-exec).  The last
+    candidate's failure is raised.  Test hook: LSD_TEST_HOOKS=1 with
+    LSD_TEST_SELFTEST_FAIL=<global rank> fails that rank's self-test of the
+    first candidate."""
+    import os
+
+    reasons: List[str] = []
+    for i, kind in enumerate(chain):
+        last = i == len(chain) - 1
+        try:
+            t = make_dist_transport(num_stages, kind, device, replicas, timeout_s, loop_ring_bytes,
+                                    warmup=False)
+        except TransportError as e:  # agreed: raised on every rank
+            if last:
+                raise
+            reasons.append(f"{kind}: {e}")
+            continue
+        err = selftest_data_plane(t, device, float(os.environ.get("LSD_SELFTEST_S", "60")))
+        if (i == 0 and err is None and os.environ.get("LSD_TEST_HOOKS") == "1"
+                and os.environ.get("LSD_TEST_SELFTEST_FAIL") == str(t.grank)):
+            err = f"rank {t.grank}: injected self-test failure (LSD_TEST_SELFTEST_FAIL)"
+        try:
+            t.agree(err, f"{kind} self-test")
+        except TransportError as e:
+            _teardown_failed(t, device)
+            if last:
+                raise
+            reasons.append(f"{kind}: {e}")
+            continue
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        t.barrier()
+        return t, kind, ("; ".join(reasons) or None)
+    raise TransportError("empty transport chain")

@@ -40,8 +40,8 @@ from ..config import EngineConfig, SamplingParams
 from ..utils import racecheck
 from ..models.stage import StageModel
 from ..parallel.comm import (DeviceLoopFabric, GlooPlanChannel, LocalFabric, LocalPlanChannel,
-                             Transport, TransportError, init_distributed, make_dist_transport,
-                             make_plan_channel)
+                             Transport, TransportError, init_distributed, make_plan_channel,
+                             open_data_plane, transport_chain)
 from ..parallel.partition import make_alt_unit_plans, make_unit_plan, union_plan, units_to_layers
 from ..parallel.pipeline import StageWorker
 from .kv_cache import KVCache, SlotAllocator, plan_slots
@@ -122,6 +122,9 @@ class Engine(racecheck.Shared):
         self._hostprof = [0.0, 0.0, 0.0, 0, 0, 0.0, 0.0, 0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
         self.kv_slots = 0
         self._stall_after: Optional[int] = None  # test hook, see _test_stall
+        # dist mode: the data plane in use and why the preferred one was left
+        self.transport_kind: Optional[str] = None
+        self.transport_fallback: Optional[str] = None
 
         if mode == "local":
             if devices is None:
@@ -160,23 +163,30 @@ class Engine(racecheck.Shared):
             import torch.distributed as dist
 
             dev = resolve_device(cfg.device)
-            kind = cfg.transport if cfg.transport not in ("auto", "local") else (
-                "nccl" if dev.type == "cuda" else "gloo")
-            init_distributed("nccl" if kind == "nccl" else "gloo", dev.type, cfg.round_timeout_s)
+            # default group: gloo (control plane) unless the chain is torch's
+            # RCCL groups alone; a fallback to "nccl" makes its own groups
+            pre = transport_chain(cfg.transport, dev.type)
+            init_distributed("nccl" if pre == ["nccl"] else "gloo", dev.type, cfg.round_timeout_s)
             self.rank = dist.get_rank()
             if dev.type == "cuda":
                 dev = torch.device("cuda", torch.cuda.current_device())
             self.devices = [dev]
-            self.transport = make_dist_transport(self.P, kind, dev, self.R, cfg.round_timeout_s,
-                                                 loop_ring_bytes=self._loop_ring_bytes())
+            shared = dev.type == "cuda" and _ranks_sharing_device(dev, None) > 1
+            chain = transport_chain(cfg.transport, dev.type, shared)
+            self.transport, self.transport_kind, self.transport_fallback = open_data_plane(
+                chain, self.P, dev, self.R, cfg.round_timeout_s, loop_ring_bytes=self._loop_ring_bytes())
+            if self.transport_fallback and self.rank == 0:
+                log.warning("data plane %s failed its self-test; running on %s (%s)", chain[0],
+                            self.transport_kind, self.transport_fallback)
             self.replica, self.stage_idx = self.transport.replica, self.transport.rank
             if os.environ.get("LSD_TEST_STALL_RANK") == str(self.rank):
                 self._stall_after = int(os.environ.get("LSD_TEST_STALL_AFTER", "0"))
             self.kv_slots = self._kv_slots([dev], collective=True)
             stage = self._build_stage(self.stage_idx, dev)
-            if os.environ.get("LSD_TEST_CORRUPT_RANK") == str(self.rank):
-                # test hook: a faulty stage (doubled norm gains) whose output
-                # must fail bench.py's token check against one GPU
+            if os.environ.get("LSD_TEST_HOOKS") == "1" and os.environ.get("LSD_TEST_CORRUPT_RANK") == str(self.rank):
+                # test hook (needs LSD_TEST_HOOKS=1): a faulty stage (doubled
+                # norm gains) whose output must fail bench.py's token check
+                log.warning("LSD_TEST_CORRUPT_RANK: rank %d doubles its norm gains (test hook)", self.rank)
                 for k, t in stage.w.items():
                     if k.endswith(("ln_1.weight", "ln_2.weight", "layernorm.weight")):
                         t.mul_(2.0)
@@ -277,21 +287,7 @@ class Engine(racecheck.Shared):
         return fits
 
     def _ranks_sharing_device(self, dev: torch.device) -> int:
-        """Dist ranks bound to this very GPU (the single-GPU rehearsal puts
-        several on one): every rank publishes (host, device identity) on the
-        control group and counts its own key.  Independent of how many GPUs
-        each process sees (HIP_VISIBLE_DEVICES) and of the node count."""
-        import socket
-
-        import torch.distributed as dist
-
-        props = torch.cuda.get_device_properties(dev)
-        ident = str(getattr(props, "uuid", "") or "") or ":".join(
-            str(getattr(props, f, "")) for f in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
-        key = (socket.gethostname(), ident if ident.strip(":") else str(dev))
-        keys = [None] * dist.get_world_size()
-        dist.all_gather_object(keys, key, group=self.transport.ctrl)
-        return max(1, sum(1 for k in keys if k == key))
+        return _ranks_sharing_device(dev, self.transport.ctrl)
 
     def _devloop_fabric(self, dev: torch.device) -> DeviceLoopFabric:
         """Loopback channels sized for the largest message an edge carries:
@@ -784,6 +780,24 @@ class Engine(racecheck.Shared):
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
             return out
+
+
+def _ranks_sharing_device(dev: torch.device, group) -> int:
+    """Dist ranks bound to this very GPU (the single-GPU rehearsal puts
+    several on one): every rank publishes (host, device identity) on `group`
+    (None: the default group) and counts its own key.  Independent of how
+    many GPUs each process sees (HIP_VISIBLE_DEVICES) and of the node count."""
+    import socket
+
+    import torch.distributed as dist
+
+    props = torch.cuda.get_device_properties(dev)
+    ident = str(getattr(props, "uuid", "") or "") or ":".join(
+        str(getattr(props, f, "")) for f in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    key = (socket.gethostname(), ident if ident.strip(":") else str(dev))
+    keys = [None] * dist.get_world_size()
+    dist.all_gather_object(keys, key, group=group)
+    return max(1, sum(1 for k in keys if k == key))
 
 
 def _with_index(dev: torch.device) -> torch.device:

@@ -49,10 +49,64 @@ def test_gloo_bench_reports_token_check(world):
 
 
 def test_gloo_bench_corrupted_stage_fails():
-    r, out = _bench(2, CPU, env_extra={"LSD_TEST_CORRUPT_RANK": "1"})
+    r, out = _bench(2, CPU, env_extra={"LSD_TEST_HOOKS": "1", "LSD_TEST_CORRUPT_RANK": "1"})
     assert r.returncode != 0, r.stdout[-2000:]
     assert out is not None and out["pipeline_matches_1gpu"] is False, out
     assert out["check_mismatched_seqs"] > 0
+
+
+def test_gloo_selftest_failure_falls_back_in_process():
+    """The data plane's startup self-test fails on one rank (injected): every
+    rank agrees, tears the first transport down and brings up the next one of
+    the chain in the same processes; the run then reports the transport it
+    used, why it left the first, and its tokens still match one stage."""
+    cpu = [a for a in CPU if a != "gloo"]
+    cpu[cpu.index("--transport") + 1:cpu.index("--transport") + 1] = ["gloo,gloo"]
+    r, out = _bench(2, cpu, env_extra={"LSD_TEST_HOOKS": "1", "LSD_TEST_SELFTEST_FAIL": "1"})
+    assert r.returncode == 0 and out is not None, r.stderr[-3000:]
+    assert out["transport"] == "gloo" and "injected" in (out["transport_fallback"] or ""), out
+    assert out["pipeline_matches_1gpu"] is True, out
+
+
+def test_gloo_selftest_pass_reports_no_fallback():
+    r, out = _bench(2, CPU)
+    assert r.returncode == 0 and out is not None, r.stderr[-3000:]
+    assert out["transport"] == "gloo" and out["transport_fallback"] is None, out
+
+
+def test_transport_chain_defaults():
+    from llm_sharding_demo_amd.parallel.comm import transport_chain
+
+    assert transport_chain("auto", "cuda") == ["rccl", "nccl"]
+    assert transport_chain("auto", "cuda", shared_gpu=True) == ["devloop", "gloo"]
+    assert transport_chain("auto", "cpu") == ["gloo"]
+    assert transport_chain("rccl,nccl", "cuda") == ["rccl", "nccl"]
+    assert transport_chain("nccl", "cuda") == ["nccl"]
+
+
+@pytest.mark.gpu
+def test_devloop_selftest_failure_falls_back_to_gloo():
+    """Two rank processes on one MI355X: the device-loopback data plane
+    passes its own eager + graph-captured self-test, a failure injected on
+    rank 1 makes both ranks abort it and fall back to host-staged gloo in
+    process; tokens still match one GPU."""
+    r, out = _bench(2, ["--model", "gpt2", "--batch", "16", "--prompt", "16", "--gen", "8",
+                        "--transport", "devloop,gloo"],
+                    env_extra={"LSD_LOOP_RING_MB": "16", "LSD_TEST_HOOKS": "1", "LSD_TEST_SELFTEST_FAIL": "1"})
+    assert r.returncode == 0 and out is not None, (r.stdout[-2000:], r.stderr[-3000:])
+    assert out["transport"] == "gloo" and "injected" in (out["transport_fallback"] or ""), out
+    assert out["pipeline_matches_1gpu"] is True, out
+
+
+@pytest.mark.gpu
+def test_auto_transport_ranks_on_one_gpu_take_devloop():
+    """Default flags with two ranks on one GPU: the auto chain detects the
+    shared device and runs the device loopback plane (self-test passed)."""
+    r, out = _bench(2, ["--model", "gpt2", "--batch", "16", "--prompt", "16", "--gen", "8"],
+                    env_extra={"LSD_LOOP_RING_MB": "16"})
+    assert r.returncode == 0 and out is not None, (r.stdout[-2000:], r.stderr[-3000:])
+    assert out["transport"] == "devloop" and out["transport_fallback"] is None, out
+    assert out["pipeline_matches_1gpu"] is True, out
 
 
 @pytest.mark.gpu
