@@ -1,24 +1,21 @@
-// hipBLASLt for the prefill projections whose epilogue the library fuses.
-//
-// Prefill GEMMs are large (GPT-2 XL: 32-64 K tokens x 1600-6400 columns).
-// The hand-written 256x256 kernel (gemm.hip gemm_p8_kernel) reaches ~1.0 PF/s
-// with its fused epilogues; hipBLASLt's tuned kernels reach 1.2-1.35 on the
-// same shapes (profiles/r3_p8_buffer_lds.log).  Two of the four projections
-// per layer need nothing the library cannot do itself, so they go there:
+// hipBLASLt as an opt-in A/B oracle (ops/routing.py `blaslt=1`; off by
+// default: every hot-path GEMM runs on the hand-written kernels of
+// csrc/kernels).  It runs the projections whose epilogue the library fuses:
 //   * MLP-up: y = gelu_new(a @ w^T + b), bf16 out      (HIPBLASLT_EPILOGUE_GELU_BIAS)
 //   * residual projections: x += a @ w^T + b, fp32 x   (beta = 1 with C = D = x,
 //     HIPBLASLT_EPILOGUE_BIAS; bf16 A / B, fp32 C / D)
-// QKV (its epilogue scatters K / V into the paged cache) stays on the
-// hand-written kernels except Llama-3 8B's 512-row decode QKV, which runs here
-// with fp32 output and a separate RoPE / cache-append pass (blaslt_f32); the
-// other decode GEMMs stay hand-written.  Row-major y[M, N] = a[M, K] w[N, K]^T is
-// the column-major D[N, M] = op_T(W[K, N]) B[K, M]: transa = T, m = N, n = M.
-// The bias runs along D's rows (our columns) as the epilogue expects.
+//   * a plain fp32-out GEMM (blaslt_f32) for the QKV comparison, whose RoPE /
+//     cache append then runs as kernels/elementwise.hip qkv_post.
+// Row-major y[M, N] = a[M, K] w[N, K]^T is the column-major D[N, M] =
+// op_T(W[K, N]) B[K, M]: transa = T, m = N, n = M; the bias runs along D's
+// rows (our columns) as the epilogue expects.
 //
-// One handle and heuristic cache per device, a workspace per microbatch lane
-// (the lanes' GEMMs run concurrently; decode calls are graph-captured, and a
-// lane's captures and replays share its workspace); the first call of a
-// (M, N, K, epilogue) asks the heuristic and keeps its first algorithm.
+// One handle and heuristic cache per device.  Only workspace-free algorithms
+// are accepted, so GEMMs issued concurrently -- two lanes of a stage, or the
+// stages of a one-GPU multi-stage rehearsal on their own streams, eager or
+// graph-captured -- share no scratch memory.  The plan cache is bounded
+// (descriptors destroyed when it overflows: prefill M varies with the chunk
+// token count) and the fp32 copy of a residual bias is made once per weight.
 // The bindings report "no algorithm" (None / false, nothing issued) and the
 // caller then keeps the hand-written kernel.
 #include <torch/extension.h>
@@ -39,7 +36,7 @@ void lt_check(hipblasStatus_t s, const char* what) {
   if (s != HIPBLAS_STATUS_SUCCESS) throw std::runtime_error(std::string("hipBLASLt ") + what + " failed: " + std::to_string((int)s));
 }
 
-constexpr size_t kWorkspace = 64ull << 20;
+constexpr size_t kMaxPlans = 256;
 
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
@@ -50,20 +47,26 @@ struct Plan {
 
 struct DeviceState {
   hipblasLtHandle_t handle = nullptr;
-  std::map<int, torch::Tensor> workspace;  // per microbatch lane: lanes run concurrently
   std::map<std::tuple<long, long, long, int, int>, Plan> plans;  // (M, N, K, epilogue, fp32 out)
+  std::map<std::pair<const void*, long>, torch::Tensor> bias32;  // fp32 copies of residual biases
 };
 
 std::mutex g_mu;
 std::map<int, DeviceState> g_dev;
 
-DeviceState& state(const torch::Tensor& like, int lane) {
+DeviceState& state(const torch::Tensor& like) {
   const int dev = like.get_device();
   auto& s = g_dev[dev];
   if (!s.handle) lt_check(hipblasLtCreate(&s.handle), "create");
-  if (!s.workspace.count(lane))
-    s.workspace[lane] = torch::empty({(long)kWorkspace}, like.options().dtype(torch::kUInt8));
   return s;
+}
+
+void destroy(Plan& p) {
+  if (p.desc) hipblasLtMatmulDescDestroy(p.desc);
+  if (p.la) hipblasLtMatrixLayoutDestroy(p.la);
+  if (p.lb) hipblasLtMatrixLayoutDestroy(p.lb);
+  if (p.lc) hipblasLtMatrixLayoutDestroy(p.lc);
+  p = Plan{};
 }
 
 // The plan for y[M, N] (bf16, or fp32 accumulated into C = D) = a[M, K] w[N, K]^T
@@ -71,6 +74,10 @@ Plan& plan(DeviceState& s, long M, long N, long K, hipblasLtEpilogue_t epi, bool
   auto key = std::make_tuple(M, N, K, (int)epi, (int)f32out);
   auto it = s.plans.find(key);
   if (it != s.plans.end()) return it->second;
+  if (s.plans.size() >= kMaxPlans) {  // bounded: drop every plan (the stream order keeps
+    for (auto& kv : s.plans) destroy(kv.second);  // earlier enqueued GEMMs valid: the
+    s.plans.clear();                              // library copies what it needs at launch)
+  }
   Plan p;
   lt_check(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F), "desc");
   const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
@@ -86,7 +93,7 @@ Plan& plan(DeviceState& s, long M, long N, long K, hipblasLtEpilogue_t epi, bool
   lt_check(hipblasLtMatrixLayoutCreate(&p.lc, f32out ? HIP_R_32F : HIP_R_16BF, N, M, N), "layout C");
   hipblasLtMatmulPreference_t pref;
   lt_check(hipblasLtMatmulPreferenceCreate(&pref), "preference");
-  const uint64_t ws = kWorkspace;
+  const uint64_t ws = 0;  // workspace-free algorithms only (see the header)
   lt_check(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws)),
            "workspace");
   hipblasLtMatmulHeuristicResult_t res[1];
@@ -95,7 +102,7 @@ Plan& plan(DeviceState& s, long M, long N, long K, hipblasLtEpilogue_t epi, bool
       hipblasLtMatmulAlgoGetHeuristic(s.handle, p.desc, p.la, p.lb, p.lc, p.lc, pref, 1, res, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   if (hs == HIPBLAS_STATUS_SUCCESS && n > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS &&
-      res[0].workspaceSize <= kWorkspace) {
+      res[0].workspaceSize == 0) {
     p.algo = res[0].algo;
     p.ok = true;
   }
@@ -117,14 +124,14 @@ const void* bias_ptr(const c10::optional<torch::Tensor>& bias, long N) {
 }
 
 void run(DeviceState& s, Plan& p, const void* bias, const torch::Tensor& a, const torch::Tensor& w,
-         float beta, void* cd, int lane) {
+         float beta, void* cd) {
   if (bias)
     lt_check(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)),
              "bias pointer");
   const float alpha = 1.f;
   auto st = at::hip::getCurrentHIPStream().stream();
   lt_check(hipblasLtMatmul(s.handle, p.desc, &alpha, w.data_ptr(), p.la, a.data_ptr(), p.lb, &beta, cd, p.lc, cd,
-                           p.lc, &p.algo, s.workspace.at(lane).data_ptr(), kWorkspace, st),
+                           p.lc, &p.algo, nullptr, 0, st),
            "matmul");
 }
 
@@ -143,11 +150,11 @@ void lsd_register_blaslt(pybind11::module& m) {
     const hipblasLtEpilogue_t epi = act == 1 ? (b ? HIPBLASLT_EPILOGUE_GELU_BIAS : HIPBLASLT_EPILOGUE_GELU)
                                              : (b ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT);
     std::lock_guard<std::mutex> lk(g_mu);
-    auto& s = state(a, (int)lane);
+    auto& s = state(a);
     auto& p = plan(s, M, N, K, epi, false);
     if (!p.ok) return c10::nullopt;
     auto y = torch::empty({M, N}, a.options());
-    run(s, p, b, a, w, 0.f, y.data_ptr(), (int)lane);
+    run(s, p, b, a, w, 0.f, y.data_ptr());
     return y;
   }, py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("lane") = 0);
   // y = a @ w^T, fp32 [M, N] (no bias: the caller's pass adds it -- the QKV
@@ -157,11 +164,11 @@ void lsd_register_blaslt(pybind11::module& m) {
     const c10::DeviceGuard guard(a.device());
     const long M = a.size(0), N = w.size(0), K = a.size(1);
     std::lock_guard<std::mutex> lk(g_mu);
-    auto& s = state(a, (int)lane);
+    auto& s = state(a);
     auto& p = plan(s, M, N, K, HIPBLASLT_EPILOGUE_DEFAULT, true);
     if (!p.ok) return c10::nullopt;
     auto y = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
-    run(s, p, nullptr, a, w, 0.f, y.data_ptr(), (int)lane);
+    run(s, p, nullptr, a, w, 0.f, y.data_ptr());
     return y;
   }, py::arg("a"), py::arg("w"), py::arg("lane") = 0);
   // x += a @ w^T + bias (x fp32 [M, N], in place); false when the library has
@@ -173,15 +180,22 @@ void lsd_register_blaslt(pybind11::module& m) {
     const long M = a.size(0), N = w.size(0), K = a.size(1);
     TORCH_CHECK(x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() == 2 && x.size(0) == M &&
                 x.size(1) == N, "blaslt_residual: x must be contiguous fp32 [M, N]");
-    bias_ptr(bias, N);  // checks
-    torch::Tensor b32;
-    if (bias.has_value()) b32 = bias->to(torch::kFloat32);
-    const void* b = bias.has_value() ? b32.data_ptr() : nullptr;
+    const void* bb = bias_ptr(bias, N);  // checks
     std::lock_guard<std::mutex> lk(g_mu);
-    auto& s = state(a, (int)lane);
+    auto& s = state(a);
+    const void* b = nullptr;
+    if (bb) {  // fp32 copy of the (persistent) bias, made once
+      auto key = std::make_pair(bb, N);
+      auto it = s.bias32.find(key);
+      if (it == s.bias32.end()) {
+        if (s.bias32.size() >= 1024) s.bias32.clear();
+        it = s.bias32.emplace(key, bias->to(torch::kFloat32)).first;
+      }
+      b = it->second.data_ptr();
+    }
     auto& p = plan(s, M, N, K, b ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT, true);
     if (!p.ok) return false;
-    run(s, p, b, a, w, 1.f, x.data_ptr(), (int)lane);
+    run(s, p, b, a, w, 1.f, x.data_ptr());
     return true;
   }, py::arg("a"), py::arg("w"), py::arg("bias"), py::arg("x"), py::arg("lane") = 0);
 }

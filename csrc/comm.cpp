@@ -2,10 +2,11 @@
 //
 // The reference moves hidden states between shards as JSON over HTTP
 // (`server.py:169-181`).  Here a pipeline edge (stage i -> i+1, and the
-// token-id return edge P-1 -> 0) is a 2-rank RCCL communicator.  Its
-// ncclSend / ncclRecv are enqueued directly on a HIP stream of the caller's
-// choosing (the edge's comm stream, ordered against the compute lanes with
-// hipEvents by parallel/comm.py RcclTransport), so they are device-async.
+// token-id return edge P-1 -> 0) gets one 2-rank RCCL communicator per
+// microbatch lane.  Its ncclSend / ncclRecv are enqueued on the CURRENT
+// stream -- the lane's stream, eagerly or inside the lane's hipGraph capture
+// (parallel/comm.py RcclTransport) -- so they are device-async and ordered
+// by the lane's own stream order, with no comm stream or event hop.
 //
 // RCCL is resolved at run time from the librccl.so.1 that torch already
 // loaded (dlopen RTLD_NOLOAD): one RCCL instance per process, the same one

@@ -3,8 +3,9 @@
 // The gate_up weight is stored in 32-row blocks [gate 16 | up 16]
 // (ops/hip.py interleave_gate_up), so the fused GEMM epilogue (gemm.hip
 // EPI_SILU_MUL) pairs each gate column with the up column 16 to its right.
-// When the GEMM itself runs elsewhere (hipBLASLt at 512 decode rows,
-// csrc/blaslt.cpp) its bf16 output [M, 2F] goes through this pass: one thread
+// When the GEMM itself runs elsewhere (the hipBLASLt A/B oracle, LSD_ROUTING
+// blaslt=1: 64-128 decode rows, csrc/blaslt.cpp) its bf16 output [M, 2F]
+// goes through this pass: one thread
 // per 8 outputs, 16-byte loads of the gate and up chunks, fp32 math, one
 // 16-byte store -- out[m, 16 j + i] = silu(y[m, 32 j + i]) * y[m, 32 j + 16 + i].
 #include "common.h"

@@ -16,9 +16,12 @@
 // (no overwrite of unread data), then release-stores head = k + 1; reader i
 // acquire-loads head, copies the slot and release-stores cursor[i] = k + 1.
 // Waits spin briefly, then sleep with backoff, and give up at their timeout.
-// The producer stores its pid in the header: a reader whose wait times out can
-// tell a quiet producer from a dead one (producer_alive), and close_ring()
-// ends every reader's wait once the ring is drained.
+// The producer stores its pid (and its pid namespace) in the header: a reader
+// whose wait times out can tell a quiet producer from a dead one
+// (producer_alive; a reader in another pid namespace -- another container of
+// the pod sharing /dev/shm -- cannot signal-probe that pid and takes the
+// producer as alive, relying on close_ring()), and close_ring() ends every
+// reader's wait once the ring is drained.
 #pragma once
 
 #include <signal.h>
@@ -69,6 +72,7 @@ class ShmRing {
     h->head.store(0, std::memory_order_relaxed);
     h->closed.store(0, std::memory_order_relaxed);
     h->producer_pid.store((int64_t)getpid(), std::memory_order_relaxed);
+    h->producer_pidns = pid_ns();
     for (int i = 0; i < kMaxReaders; ++i) h->cursor[i].v.store(0, std::memory_order_relaxed);
     // publishes the geometry above: attach() acquire-loads the magic first
     h->magic.store(kMagic, std::memory_order_release);
@@ -140,7 +144,14 @@ class ShmRing {
   // Is the producing process still there?  (EPERM: alive, owned by another user.)
   bool producer_alive() const {
     const pid_t pid = (pid_t)hdr_->producer_pid.load(std::memory_order_relaxed);
+    const uint64_t ns = hdr_->producer_pidns;
+    if (ns == 0 || ns != pid_ns()) return true;  // not our pid namespace: no probe possible
     return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM);
+  }
+  // Inode of this process's pid namespace (0 when /proc does not tell).
+  static uint64_t pid_ns() {
+    struct stat st;
+    return stat("/proc/self/ns/pid", &st) == 0 ? (uint64_t)st.st_ino : 0;
   }
   uint64_t head() const { return hdr_->head.load(std::memory_order_acquire); }
   uint64_t cursor(int i) const { return hdr_->cursor[i].v.load(std::memory_order_acquire); }
@@ -155,6 +166,7 @@ class ShmRing {
     std::atomic<uint64_t> magic;
     uint32_t slots, slot_bytes, readers, pad;
     std::atomic<int64_t> producer_pid;
+    uint64_t producer_pidns;  // written before the magic's release store
     alignas(64) std::atomic<uint64_t> head;
     alignas(64) std::atomic<uint64_t> closed;
     Counter cursor[kMaxReaders];

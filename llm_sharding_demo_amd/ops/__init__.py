@@ -6,8 +6,10 @@ stage) is written once against the `Backend` interface below.  Two implementatio
 * `ReferenceBackend` -- plain PyTorch in fp32 (ops/reference.py).  Used on CPU
   (tests, golden numerics, the tiny-gpt2 reference config).
 * `HipBackend` (ops/hip.py) -- the hand-written CDNA4 kernels in
-  csrc/kernels/*.hip.  Used for every tensor on a GPU.  There is no silent
-  fallback: if the extension is missing on a GPU box, `get_backend` raises.
+  csrc/kernels/*.hip, routed by one table (ops/routing.py).  Used for every
+  tensor on a GPU; hipBLASLt only runs when an A/B run asks for it
+  (LSD_ROUTING=blaslt=1).  There is no silent fallback: if the extension is
+  missing on a GPU box, `get_backend` raises.
 
 Residual stream convention: the residual `x` is fp32 [T, H].  GEMMs whose
 epilogue is "add into the residual" may split K across workgroups; their

@@ -715,7 +715,7 @@ class Watchdog:
             elapsed = time.monotonic() - started
             if elapsed > self.timeout:
                 self._fire("WatchdogTimeout",
-                           f"no pipeline progress for {elapsed:.0f} s (deadline {self.timeout:.0f} s)")
+                           f"no pipeline progress for {elapsed:.3g} s (deadline {self.timeout:.3g} s)")
 
     def _fire(self, kind: str, msg: str) -> None:
         self.fired = True

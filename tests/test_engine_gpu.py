@@ -52,7 +52,7 @@ def test_wide_decode_batch_on_ring_gemms_matches_cpu_golden(model):
 
     from llm_sharding_demo_amd.ops.hip import HipBackend
 
-    assert HipBackend._tiled(200, 64) and HipBackend.TILED3_MAX > 0
+    assert HipBackend._tiled(200, 64) and HipBackend.R.tiled3_max > 0
     mc = get_model_config(model)
     w = full_weights(mc)
     B = 200

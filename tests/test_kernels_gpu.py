@@ -94,8 +94,8 @@ def test_norm_wave_with_slabs(C, H, rms, S, sdt):
 def _norm_defaults(C):
     from llm_sharding_demo_amd.ops.hip import HipBackend
 
-    C.norm_set_wave_min(HipBackend.NORM_WAVE_MIN)
-    C.norm_set_wave_narrow_min(HipBackend.NORM_WAVE_NARROW_MIN)
+    C.norm_set_wave_min(HipBackend.R.norm_wave_min)
+    C.norm_set_wave_narrow_min(HipBackend.R.norm_wave_narrow_min)
 
 
 @pytest.mark.parametrize("T,H", [(258, 768), (258, 1600), (4099, 768), (4099, 1600), (100, 768)])

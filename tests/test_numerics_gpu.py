@@ -92,10 +92,9 @@ def test_llama_512_row_decode_matches_fp32_golden():
     """Llama-3 8B dims (4 layers) with 512 sequences: the 512-row decode
     GEMMs of the Llama-3 8B bench (256x256 gate_up kernel with the fused
     SiLU*up epilogue) against the fp32 golden with the Llama bounds.  With
-    the hipBLASLt gate_up forced on (LSD_BLASLT_SILU_MIN_M=512) it measured
-    top-1 0.983, max 0.041, mean 0.029 (profiles/r5_llama_blaslt.log).  The
-    512-row decode QKV runs on hipBLASLt + the RoPE / cache-append pass
-    (HipBackend.BLASLT_QKV_MIN_M)."""
+    the hipBLASLt gate_up forced on it measured top-1 0.983, max 0.041, mean
+    0.029 (profiles/r5_llama_blaslt.log).  The 512-row decode QKV runs on the
+    hand-written ring kernel with the fused RoPE / cache-append epilogue."""
     from llm_sharding_demo_amd.config import get_model_config
 
     mc = dataclasses.replace(get_model_config("llama-3-8b"), n_layers=4)

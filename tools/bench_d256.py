@@ -38,7 +38,7 @@ KNOBS = {
     "big": lambda on: C.gemm_set_big_kind(2 if on else 4),          # gemm_big_kernel instead of p8
     "nop8": lambda on: C.gemm_set_big_min((1 << 30) if on else 160),  # no 256x256 kernel: 128-row tiles
     "r8": lambda on: (C.gemm_set_big_min((1 << 30) if on else 160),    # 8-wave 128x64 ring
-                      C.gemm_set_tiled3_max((1 << 30) if on else HipBackend.TILED3_MAX)),
+                      C.gemm_set_tiled3_max((1 << 30) if on else HipBackend.R.tiled3_max)),
 }
 
 
@@ -123,7 +123,7 @@ def main():
                         if act == 2:  # SiLU * up: the GEMM, then the elementwise pass
                             return C.silu_mul(C.blaslt_linear(a, w, bias, 0))
                         return C.blaslt_linear(a, w, bias, act)
-                    C.gemm_set_ring8(r8 & 15 if not isinstance(r8, str) else HipBackend.RING8)  # read at launch
+                    C.gemm_set_ring8(r8 & 15 if not isinstance(r8, str) else HipBackend.R.ring8)  # read at launch
                     C.gemm_set_ring8_flags((r8 >> 4) & 15 if not isinstance(r8, str) else 0)
                     w = ws[it[0] % nw]
                     it[0] += 1
@@ -138,7 +138,7 @@ def main():
                         if bn == 0:
                             s2 = be._resid_splits(M, N, K)
                             tiled = be._tiled(M, N)
-                            slab = C.linear_residual(a, w, bias, x, s2, tiled, cnt, tiled or be.DEFER_RESID)
+                            slab = C.linear_residual(a, w, bias, x, s2, tiled, cnt, tiled or be.R.defer_resid)
                         else:
                             slab = C.linear_residual(a, w, bias, x, S, kind, cnt, True)
                         if slab is not None:

@@ -92,7 +92,7 @@ def bench_gemm(M, N, K, act=0, resid=False, label="", force_tiled=False):
         w = ws[it[0] % len(ws)]
         it[0] += 1
         if resid:  # + the combine the engine pairs it with (deferred slabs -> norm)
-            slab = C.linear_residual(a, w, None, x, splits, tiled, be.counters, be.DEFER_RESID)
+            slab = C.linear_residual(a, w, None, x, splits, tiled, be.counters, be.R.defer_resid)
             if slab is not None:
                 C.norm(x, slab, None, None, None, 0.0, True, None, False)
         else:
@@ -284,7 +284,7 @@ def bench_ring_tn(M, H=1600, F=6400):
     """Decode-sized ring GEMMs: 128x64 vs 128x32 tiles (2 blocks/CU), rotating
     weights; residual projections with their slab combine at several splits."""
     cnt = torch.zeros(1 << 16, dtype=torch.int32, device=DEV)
-    C.gemm_set_tiled3_max(512)  # the engine's ring cap (HipBackend.TILED3_MAX)
+    C.gemm_set_tiled3_max(512)  # the engine's ring cap (Routing.tiled3_max)
     a = torch.randn(M, H, device=DEV).bfloat16()
     af = torch.randn(M, F, device=DEV).bfloat16()
     x = torch.randn(M, H, device=DEV)
@@ -581,31 +581,34 @@ def main():
             stamps_gemm(M, 1600, 1600, S, label="_proj")
         stamps_gemm(64, 50304, 1600, 1, label="_lmhead")
     H, F, V = 1600, 6400, 50304
+    from llm_sharding_demo_amd.ops.hip import HipBackend
+    R0 = HipBackend.R
+
+    def route(**kw):  # bench_gemm's HipBackend() reads the class routing table (ops/routing.py)
+        HipBackend.R = R0.replace(**kw)
+
     if "sweep" in which:
-        from llm_sharding_demo_amd.ops.hip import HipBackend
         for tgt in (128, 256, 384, 512, 768, 1024):
-            HipBackend.SK_TARGET = tgt
-            print("SK_TARGET", tgt, flush=True)
+            route(sk_target=tgt)
+            print("sk_target", tgt, flush=True)
             for M in (64, 128):
                 bench_gemm(M, 3 * H, H, label="_qkv")
                 bench_gemm(M, F, H, act=1, label="_fc")
                 bench_gemm(M, H, H, resid=True, label="_proj")
                 bench_gemm(M, H, F, resid=True, label="_proj2")
                 bench_gemm(M, V, H, label="_lmhead")
-        HipBackend.SK_TARGET = None
-    if "rows" in which:  # decode GEMM: row blocks x column tile x split target at M = 128
-        from llm_sharding_demo_amd.ops.hip import HipBackend
-        for nw2 in (128, 64):
-            for rows in (128, 64):
-                for tgt in (256, 384, 512):
-                    HipBackend.SK_ROWS, HipBackend.SK_TARGET, HipBackend.NW2_ROWS = rows, tgt, nw2
-                    tag = f"_nw{1 if nw2 >= 128 else 2}_r{rows}_t{tgt}"
-                    bench_gemm(128, 3 * H, H, label="_qkv" + tag)
-                    bench_gemm(128, F, H, act=1, label="_fc" + tag)
-                    bench_gemm(128, H, H, resid=True, label="_proj" + tag)
-                    bench_gemm(128, H, F, resid=True, label="_proj2" + tag)
-                    bench_gemm(128, V, H, label="_lmhead" + tag)
-        HipBackend.SK_ROWS, HipBackend.SK_TARGET, HipBackend.NW2_ROWS = 64, None, 1 << 30
+        route()
+    if "rows" in which:  # decode GEMM: row blocks x split target at M = 128
+        for rows in (128, 64):
+            for tgt in (256, 384, 512):
+                route(sk_rows=rows, sk_target=tgt)
+                tag = f"_r{rows}_t{tgt}"
+                bench_gemm(128, 3 * H, H, label="_qkv" + tag)
+                bench_gemm(128, F, H, act=1, label="_fc" + tag)
+                bench_gemm(128, H, H, resid=True, label="_proj" + tag)
+                bench_gemm(128, H, F, resid=True, label="_proj2" + tag)
+                bench_gemm(128, V, H, label="_lmhead" + tag)
+        route()
     if "layer" in which:
         for M in (1, 16, 64, 128):
             bench_decode_layer(M)
@@ -616,34 +619,27 @@ def main():
         bench_gemm(128, 128256, 4096, label="_lmhead_llama")
         bench_gemm(128, 128256, 4096, label="_lmhead_llama_tiled", force_tiled=True)
     if "fc256" in which:  # one shape for PMC passes: MLP-up at 256 rows, ring / dbuf / split-K
-        from llm_sharding_demo_amd.ops.hip import HipBackend
-        t3_default, minn_default, allm_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M
-        for t3 in (1 << 30, 0):  # bench_gemm's HipBackend() applies the class knob
-            HipBackend.TILED3_MAX = t3
+        for t3 in (1 << 30, 0):
+            route(tiled3_max=t3)
             bench_gemm(256, F, H, act=1, label="_fc_tiled" + ("_ring3" if t3 else "_dbuf"), force_tiled=True)
-        HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M = t3_default, 1 << 30, 1 << 30
+        route(tiled_min_n=1 << 30, tiled_all_m=1 << 30)
         bench_gemm(256, F, H, act=1, label="_fc_sk")
-        HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M = minn_default, allm_default
+        route()
     if "tiled3" in which:  # 128x128 kernel: double buffer vs 3-slot LDS ring, decode-sized M
-        from llm_sharding_demo_amd.ops.hip import HipBackend
-        t3_default, minn_default, allm_default = HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M
         for M in (128, 256):
             for t3, slots, rtn in ((0, 3, 128), (1 << 30, 3, 128), (1 << 30, 4, 128), (1 << 30, 3, 64)):
-                # bench_gemm's HipBackend() applies the class knobs
-                HipBackend.TILED3_MAX, HipBackend.RING_SLOTS, HipBackend.RING_TN = t3, slots, rtn
+                route(tiled3_max=t3, ring_slots=slots, ring_tn=rtn)
                 tag = (f"_ring{slots}" + ("_n64" if rtn == 64 else "")) if t3 else "_dbuf"
                 if M == 128:
                     bench_gemm(M, V, H, label="_lmhead" + tag, force_tiled=True)
                 bench_gemm(M, 3 * H, H, label="_qkv_tiled" + tag, force_tiled=True)
                 bench_gemm(M, F, H, act=1, label="_fc_tiled" + tag, force_tiled=True)
                 bench_gemm(M, H, F, resid=True, label="_proj2_tiled" + tag, force_tiled=True)
-            HipBackend.TILED3_MAX, HipBackend.TILED_MIN_N, HipBackend.RING_SLOTS = t3_default, 1 << 30, 3
-            HipBackend.TILED_ALL_M = 1 << 30
-            HipBackend.RING_TN = 128
+            route(tiled_min_n=1 << 30, tiled_all_m=1 << 30, ring_tn=128)
             bench_gemm(M, 3 * H, H, label="_qkv_sk")
             bench_gemm(M, F, H, act=1, label="_fc_sk")
             bench_gemm(M, H, F, resid=True, label="_proj2_sk")
-            HipBackend.TILED_MIN_N, HipBackend.TILED_ALL_M = minn_default, allm_default
+            route()
     if "tiledsk" in which:  # split-K slabs + norm combine: decode kernel vs 128x128 tiled
         for M in (64, 128):
             for (N, K, nm) in ((3 * H, H, "qkv"), (F, H, "fc"), (H, H, "proj"), (H, F, "proj2")):
