@@ -169,7 +169,7 @@ void run_gemm(GemmParams& p, int epi, int64_t tiled, int64_t splits,
     const int r8 = tiled == 1 ? lsd_gemm_ring8_tiles(p.M, p.N, p.K, (int)splits) : 0;
     TORCH_CHECK(bn > 0 || r8 > 0, what, ": tiled split-K with an in-kernel combine needs the 256-row "
                 "kernel (kind 2 / 3) or the 8-wave decode ring");
-    const long tiles = r8 > 0 ? r8 : (p.N + bn - 1) / bn;
+    const long tiles = r8 > 0 ? r8 : (long)((p.N + bn - 1) / bn) * ((p.M + 255) / 256);
     const long tile_floats = r8 > 0 ? 128L * 64 : 256L * bn;
     TORCH_CHECK(counters.has_value(), what, ": split-K needs the ticket counter buffer");
     need(*counters, torch::kInt32, "counters");

@@ -41,6 +41,20 @@ enum Epi : int {
 };
 
 
+// (head, dim) of column c inside the q / k / v block: shifts and a mask for the
+// power-of-two head dims of every model here (a wave-uniform branch; integer
+// division by a runtime divisor is a ~40-instruction sequence per call, paid
+// for every 16-byte chunk of the prefill QKV epilogue)
+__device__ __forceinline__ void hd_split(int hd, int c, int& head, int& d) {
+  if ((hd & (hd - 1)) == 0) {
+    head = c >> __builtin_ctz(hd);
+    d = c & (hd - 1);
+  } else {
+    head = c / hd;
+    d = c % hd;
+  }
+}
+
 // Stores the 4 accumulator values of one 16x16 MFMA tile owned by this lane:
 // column n, rows row0 + i.  All lanes of the wave must call it (RoPE uses a
 // cross-lane exchange).  `v2` carries the paired tile for EPI_SILU_MUL.
@@ -101,7 +115,8 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int row0, int n, 
     for (int i = 0; i < 4; ++i) y[i] = v[i] + b;
     const int qk = p.q_size + p.kv_size;
     if (p.rope != nullptr && n < qk) {  // uniform per 16-column tile (q/k sizes are multiples of hd)
-      const int d = (n < p.q_size ? n : n - p.q_size) % p.hd;
+      int hh, d;
+      hd_split(p.hd, n < p.q_size ? n : n - p.q_size, hh, d);
       const int half = p.hd >> 1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -121,7 +136,8 @@ __device__ __forceinline__ void epilogue4(const GemmParams& p, int row0, int n, 
         reinterpret_cast<bf16*>(p.out)[(long)m * p.ldo + n] = f2bf(y[i]);
       } else {
         const int c = n < qk ? n - p.q_size : n - qk;
-        const int head = c / p.hd, d = c % p.hd;
+        int head, d;
+        hd_split(p.hd, c, head, d);
         bf16* cache = n < qk ? p.kc : p.vc;
         const long idx = (((long)p.tslot[m] * p.n_kv + head) * p.max_seq + p.tpos[m]) * p.hd + d;
         cache[idx] = f2bf(y[i]);
@@ -171,7 +187,8 @@ template <int EPI>
 __device__ __forceinline__ void epi8_pre2(const GemmParams& p, int n, Epi8Pre& e) {
   if constexpr (EPI == EPI_QKV) {
     if (p.rope != nullptr && n < p.q_size + p.kv_size) {
-      const int d0 = (n < p.q_size ? n : n - p.q_size) % p.hd;
+      int hh, d0;
+      hd_split(p.hd, n < p.q_size ? n : n - p.q_size, hh, d0);
       const f32x4* cs = reinterpret_cast<const f32x4*>(p.rope + ((long)e.pos * (p.hd >> 1) + (d0 >> 1)) * 2);
       e.cs0 = cs[0];
       e.cs1 = cs[1];
@@ -253,7 +270,9 @@ __device__ __forceinline__ void epi8_post(const GemmParams& p, int m, int n, con
     } else {
       const int c = n < qk ? n - p.q_size : n - qk;
       bf16* cache = n < qk ? p.kc : p.vc;
-      st8(cache + (((long)e.slot * p.n_kv + c / p.hd) * p.max_seq + e.pos) * p.hd + c % p.hd, o);
+      int head, d;
+      hd_split(p.hd, c, head, d);
+      st8(cache + (((long)e.slot * p.n_kv + head) * p.max_seq + e.pos) * p.hd + d, o);
     }
   }
 }
@@ -289,10 +308,12 @@ __device__ __forceinline__ void store_pass(const GemmParams& p, int nchunks, int
   // i.e. one store round trip per chunk again
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
   if constexpr (EPI == EPI_QKV) {
+    if (p.rope != nullptr) {  // wave-uniform: GPT-2 has no RoPE loads to wait for
 #pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      if (ok[i]) epi8_pre2<EPI>(p, nn[i], e[i]);
-    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+      for (int i = 0; i < NCH; ++i)
+        if (ok[i]) epi8_pre2<EPI>(p, nn[i], e[i]);
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    }
   }
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
@@ -1690,7 +1711,11 @@ __global__ __launch_bounds__(512) void gemm_d256_kernel(GemmParams p, int* __res
   const int S = p.splits;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = bid / S, split = bid % S;
-  const int n0 = tile * BN;
+  // tiles are column-major over 256-row blocks: a column tile's row blocks
+  // (and its splits) have consecutive remapped ids, so they share an XCD's L2
+  // for the W tile (speed only)
+  const int RB = (p.M + 255) / 256;
+  const int rb = tile % RB, n0 = (tile / RB) * BN, m0 = rb * 256;
   const int KT = p.K / 64;
   const int kb = (int)((long)KT * split / S), ke = (int)((long)KT * (split + 1) / S);
   const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -1705,7 +1730,7 @@ __global__ __launch_bounds__(512) void gemm_d256_kernel(GemmParams p, int* __res
 
   auto issue = [&](int kt, int slot) {
     char* b = smem + slot * SLOT_BYTES;
-    stage8<256>(b, p.A, p.lda, 0, p.M - 1, kt * 64);
+    stage8<256>(b, p.A, p.lda, m0, p.M - 1, kt * 64);
     stage8<BN>(b + A_BYTES, p.W, p.ldw, n0, p.N - 1, kt * 64);
   };
 #pragma unroll
@@ -1812,7 +1837,7 @@ __global__ __launch_bounds__(512) void gemm_d256_kernel(GemmParams p, int* __res
   if constexpr (EPI != EPI_SILU_MUL) {
     store_pass<EPI, (256 * CPR + 511) / 512, 512>(p, 256 * CPR, split, [&](int c, int& m, int& n, const float*& src) {
       const int row = c / CPR, ch = c % CPR;
-      m = row;
+      m = m0 + row;
       n = n0 + ch * 8;
       src = ct + row * CLD + ch * 8;
       return m < p.M && n < p.N;
@@ -1821,7 +1846,7 @@ __global__ __launch_bounds__(512) void gemm_d256_kernel(GemmParams p, int* __res
     return;
   }
   for (int c = threadIdx.x; c < 256 * CPR; c += 512) {
-    const int row = c / CPR, ch = c % CPR, m = row, n = n0 + ch * 8;
+    const int row = c / CPR, ch = c % CPR, m = m0 + row, n = n0 + ch * 8;
     if (m >= p.M || n >= p.N) continue;
     const float* src = ct + row * CLD + ch * 8;
     const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
@@ -1939,15 +1964,15 @@ static hipError_t launch_sk(const GemmParams& p, int* cnt, float* ws, hipStream_
 
 // Launch kinds (lsd_gemm `kind`): 0 split-K decode kernel, 1 tiled family
 // (ring / 128x128 / 256x256 by shape), 2 / 3 gemm_d256 with 64 / 128-column
-// tiles (M <= 256, K % 64 == 0; the caller picks it per GEMM).
+// tiles (M <= 1024 in 256-row blocks, K % 64 == 0; the caller picks it per GEMM).
 static int d256_bn(int kind, int M, int N, int K) {
-  if (kind < 2 || M < 1 || M > 256 || K % 64 != 0) return 0;
+  if (kind < 2 || M < 1 || M > 1024 || K % 64 != 0) return 0;
   return kind == 3 && N % 128 == 0 ? 128 : 64;
 }
 
 template <int EPI, int BN>
 static hipError_t launch_d256_bn(const GemmParams& p, int* cnt, float* ws, hipStream_t st) {
-  const dim3 grid(((p.N + BN - 1) / BN) * p.splits), block(512);
+  const dim3 grid(((p.N + BN - 1) / BN) * ((p.M + 255) / 256) * p.splits), block(512);
   const int slots = BN == 128 ? min(g_d256_slots, 3) : g_d256_slots;
   switch (slots) {
     case 2: hipLaunchKernelGGL((gemm_d256_kernel<EPI, BN, 2>), grid, block, 0, st, p, cnt, ws); break;

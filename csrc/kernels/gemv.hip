@@ -119,6 +119,31 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     const int KC = p.K >> 3;  // valid 16-byte chunks per row
     const int M = p.M;
 
+    // ---- 0. the epilogue's own operands, fetched NOW (they do not depend on
+    // the dot products): bias, the residual value the RESID epilogue adds to,
+    // the QKV rows' position / cache slot and the RoPE partner's bias.  Loaded
+    // after the reduction they cost one dependent memory round trip at the
+    // tail of every launch (the single-stream layer is five such tails).
+    constexpr int NOUT = EPI == gv::SILU ? V / 2 : V;
+    const bool epi_thread = tid < 4 * NOUT;
+    const int e_w2 = tid / NOUT, e_o = tid % NOUT;
+    const int e_j = e_o / MR, e_m = e_o % MR;
+    const int e_n = (blockIdx.x * 4 + e_w2) * CPW + e_j;  // output column (non-SiLU)
+    const bool e_live = epi_thread && e_m < M && e_n < p.N;
+    float e_bias = 0.f, e_biasp = 0.f, e_x = 0.f;
+    int e_pos = 0, e_slot = 0;
+    if constexpr (EPI != gv::SILU) {
+      if (e_live) {
+        if (p.bias) e_bias = bf2f(p.bias[e_n]);
+        if constexpr (EPI == gv::RESID) e_x = reinterpret_cast<const float*>(p.out)[(long)e_m * p.ldo + e_n];
+        if constexpr (EPI == gv::QKV) {
+          e_pos = p.tpos[e_m];
+          if (e_n >= p.q_size) e_slot = p.tslot[e_m];
+          if (CPW % 2 == 0 && p.rope != nullptr && p.bias && e_n < p.q_size + p.kv_size) e_biasp = bf2f(p.bias[e_n ^ 1]);
+        }
+      }
+    }
+
     // ---- 1. activation rows first (L2-resident: they land before the weights)
     constexpr int NV = NORM != gv::NONE ? 2 * NB : 1;  // f32x4 per thread per row
     constexpr int NA = NORM != gv::NONE ? 1 : MR * NB;  // bf16x8 copy chunks per thread
@@ -220,6 +245,18 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     }
     __syncthreads();
 
+    // the RoPE (cos, sin) of this epilogue thread's position: issued before the
+    // dot products (its position arrived with the first loads)
+    float e_cs0 = 0.f, e_cs1 = 0.f;
+    if constexpr (EPI == gv::QKV) {
+      if (CPW % 2 == 0 && p.rope != nullptr && e_live && e_n < p.q_size + p.kv_size) {
+        const int d = (e_n < p.q_size ? e_n : e_n - p.q_size) % p.hd;
+        const float* cs = p.rope + ((long)e_pos * (p.hd >> 1) + (d >> 1)) * 2;
+        e_cs0 = cs[0];
+        e_cs1 = cs[1];
+      }
+    }
+
     // ---- 4. dot products (W from registers, x from LDS)
     float acc[V];
 #pragma unroll
@@ -248,10 +285,9 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     if ((lane & (64 / V - 1)) == 0) red[w * 16 + idx] = acc[0];
     __syncthreads();
 
-    // ---- 6. fused epilogue, one thread per (wave, output)
-    constexpr int NOUT = EPI == gv::SILU ? V / 2 : V;
-    if (tid < 4 * NOUT) {
-      const int w2 = tid / NOUT, o = tid % NOUT;
+    // ---- 6. fused epilogue, one thread per (wave, output); operands prefetched in step 0
+    if (epi_thread) {
+      const int w2 = e_w2, o = e_o;
       const int gw2 = blockIdx.x * 4 + w2;
       const float* rv = red + w2 * 16;
       if constexpr (EPI == gv::SILU) {
@@ -261,35 +297,31 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
           const float g = rv[(2 * jj) * MR + m], u = rv[(2 * jj + 1) * MR + m];
           reinterpret_cast<bf16*>(p.out)[(long)m * p.ldo + col] = f2bf(silu(g) * u);
         }
-      } else {
-        const int j = o / MR, m = o % MR;
-        const int n = gw2 * CPW + j;
-        if (m < M && n < p.N) {
-          float y = rv[j * MR + m] + (p.bias ? bf2f(p.bias[n]) : 0.f);
-          if constexpr (EPI == gv::F32) {
-            reinterpret_cast<float*>(p.out)[(long)m * p.ldo + n] = y;
-          } else if constexpr (EPI == gv::RESID) {
-            reinterpret_cast<float*>(p.out)[(long)m * p.ldo + n] += y;
-          } else if constexpr (EPI == gv::BF16 || EPI == gv::GELU) {
-            reinterpret_cast<bf16*>(p.out)[(long)m * p.ldo + n] = f2bf(EPI == gv::GELU ? gelu_new(y) : y);
-          } else if constexpr (EPI == gv::QKV) {
-            const int qk = p.q_size + p.kv_size;
-            const int pos = p.tpos[m];
-            if (CPW % 2 == 0 && p.rope != nullptr && n < qk) {
-              // RoPE pairs (2i, 2i+1) are this wave's rows j, j^1 (ops/hip.py
-              // rope_pair_permutation makes the rotated pairs adjacent)
-              const float yp = rv[(j ^ 1) * MR + m] + (p.bias ? bf2f(p.bias[n ^ 1]) : 0.f);
-              const int d = (n < p.q_size ? n : n - p.q_size) % p.hd;
-              const float* cs = p.rope + ((long)pos * (p.hd >> 1) + (d >> 1)) * 2;
-              y = (d & 1) ? (y * cs[0] + yp * cs[1]) : (y * cs[0] - yp * cs[1]);
-            }
-            if (n < p.q_size) {
-              reinterpret_cast<bf16*>(p.out)[(long)m * p.ldo + n] = f2bf(y);
-            } else {
-              const int c = n < qk ? n - p.q_size : n - qk;
-              bf16* cache = n < qk ? p.kc : p.vc;
-              cache[(((long)p.tslot[m] * p.n_kv + c / p.hd) * p.max_seq + pos) * p.hd + c % p.hd] = f2bf(y);
-            }
+      } else if (e_live) {
+        const int j = e_j, m = e_m, n = e_n;
+        float y = rv[j * MR + m] + e_bias;
+        if constexpr (EPI == gv::F32) {
+          reinterpret_cast<float*>(p.out)[(long)m * p.ldo + n] = y;
+        } else if constexpr (EPI == gv::RESID) {
+          reinterpret_cast<float*>(p.out)[(long)m * p.ldo + n] = e_x + y;
+        } else if constexpr (EPI == gv::BF16 || EPI == gv::GELU) {
+          reinterpret_cast<bf16*>(p.out)[(long)m * p.ldo + n] = f2bf(EPI == gv::GELU ? gelu_new(y) : y);
+        } else if constexpr (EPI == gv::QKV) {
+          const int qk = p.q_size + p.kv_size;
+          const int pos = e_pos;
+          if (CPW % 2 == 0 && p.rope != nullptr && n < qk) {
+            // RoPE pairs (2i, 2i+1) are this wave's rows j, j^1 (ops/hip.py
+            // rope_pair_permutation makes the rotated pairs adjacent)
+            const float yp = rv[(j ^ 1) * MR + m] + e_biasp;
+            const int d = (n < p.q_size ? n : n - p.q_size) % p.hd;
+            y = (d & 1) ? (y * e_cs0 + yp * e_cs1) : (y * e_cs0 - yp * e_cs1);
+          }
+          if (n < p.q_size) {
+            reinterpret_cast<bf16*>(p.out)[(long)m * p.ldo + n] = f2bf(y);
+          } else {
+            const int c = n < qk ? n - p.q_size : n - qk;
+            bf16* cache = n < qk ? p.kc : p.vc;
+            cache[(((long)e_slot * p.n_kv + c / p.hd) * p.max_seq + pos) * p.hd + c % p.hd] = f2bf(y);
           }
         }
       }

@@ -476,8 +476,7 @@ class StageWorker(racecheck.Shared):
             # the native path posts every receive in stream order itself: no
             # look-ahead posting of the next step's first receive
             following = []
-        if self._merged_prefill(plan, items):
-            return
+        items = self._merged_prefill(plan, items)
         if items:
             self._post(items[0])
         for i, gp in enumerate(items):
@@ -485,23 +484,29 @@ class StageWorker(racecheck.Shared):
             with self.on_lane(gp.g), trace_range(f"stage{self.r}/step{plan.step}/g{gp.g}"):
                 self._item(plan, gp, nx)
 
-    # One stage: the prefill items of a step in which every group only joins
-    # sequences (a session start) run as ONE forward over all their chunks on
-    # the first item's lane -- GEMMs of every group's rows together instead of
-    # one per group on concurrent lanes; each group's sampled first tokens go
-    # to its own token-return vector and the other lanes wait for the work.
-    # GPT-2 XL headline: prefill 209-210 -> 198 ms (65 K-row GEMMs, MLP-up on
-    # hipBLASLt from 64 K rows), GPT-2 small 21.2 -> 18.8 ms
+    # One stage: the prefill-only items of a step (groups that only join
+    # sequences this step: no decode rows, no readout of earlier rows) run as
+    # ONE forward over all their chunks on the first such item's lane -- GEMMs
+    # of those groups' rows together instead of one per group on concurrent
+    # lanes; each group's sampled first tokens go to its own token-return
+    # vector and the other lanes wait for the work.  Items with decode rows
+    # run as usual after it.  GPT-2 XL headline (every group joins at the
+    # session start): prefill 209-210 -> 198 ms, GPT-2 small 21.2 -> 18.8 ms
     # (profiles/r5_merge_prefill.log); LSD_MERGE_PREFILL=0 keeps one item per group.
     MERGE_PREFILL = os.environ.get("LSD_MERGE_PREFILL", "1") == "1"
 
-    def _merged_prefill(self, plan: StepPlan, items: List[GroupPlan]) -> bool:
+    def _merged_prefill(self, plan: StepPlan, items: List[GroupPlan]) -> List[GroupPlan]:
+        """Run the step's prefill-only items merged (>= 2 of them, one stage);
+        returns the items still to run."""
         if not (getattr(self, "merge_prefill", self.MERGE_PREFILL) and self.P == 1 and len(items) > 1
                 and self.device.type == "cuda"):
-            return False
-        if any(gp.kind == "fwd_b" or not gp.chunks or gp.b > 0 or gp.rows is not None or gp.ret > 0
-               for gp in items):
-            return False
+            return items
+        pure = [gp for gp in items if gp.kind != "fwd_b" and gp.chunks and gp.b == 0 and gp.rows is None
+                and gp.ret == 0]
+        if len(pure) < 2:
+            return items
+        rest = [gp for gp in items if not any(gp is q for q in pure)]
+        items = pure
         import types
 
         g0 = items[0].g
@@ -524,7 +529,7 @@ class StageWorker(racecheck.Shared):
             ev.record()
         for lane in {self.lane_of(gp.g) for gp in items} - {self.lane_of(g0)}:
             self.lanes[lane].wait_event(ev)
-        return True
+        return rest
 
     def _new_event(self, timing: bool) -> torch.cuda.Event:
         """A created (recorded once) event whose raw handle C++ can record

@@ -88,11 +88,11 @@ def test_graphs_equal_eager(model):
 
 
 def test_graphs_equal_eager_blaslt_silu(monkeypatch):
-    """Decode gate_up on hipBLASLt + the SiLU*up pass (forced from 1 row; the
-    default is 512) inside captured decode graphs gives the eager tokens."""
+    """Decode gate_up on hipBLASLt + the SiLU*up pass (the A/B oracle route,
+    forced from 1 row) inside captured decode graphs gives the eager tokens."""
     from llm_sharding_demo_amd.ops.hip import HipBackend
 
-    monkeypatch.setattr(HipBackend, "BLASLT_SILU_MIN_M", 1)
+    monkeypatch.setattr(HipBackend, "R", HipBackend.R.replace(blaslt=1, blaslt_silu_min_m=1))
     prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 50))]
     sp = SamplingParams(greedy=True, max_new_tokens=12)
     a = _engine("llama-test", graphs=False).generate_ids(prompts, sp)
@@ -102,19 +102,37 @@ def test_graphs_equal_eager_blaslt_silu(monkeypatch):
 
 
 def test_graphs_equal_eager_blaslt_qkv(monkeypatch):
-    """Decode QKV on hipBLASLt + the RoPE / cache-append pass (forced from 1
-    row and any K; the default is 512 rows with K >= 4096) inside captured
-    decode graphs gives the eager tokens."""
+    """Decode QKV on hipBLASLt + the RoPE / cache-append pass (the A/B oracle
+    route, forced from 1 row and any K) inside captured decode graphs gives
+    the eager tokens."""
     from llm_sharding_demo_amd.ops.hip import HipBackend
 
-    monkeypatch.setattr(HipBackend, "BLASLT_QKV_MIN_M", 1)
-    monkeypatch.setattr(HipBackend, "BLASLT_QKV_MIN_K", 1)
+    monkeypatch.setattr(HipBackend, "R", HipBackend.R.replace(blaslt=1, blaslt_qkv_min_m=1, blaslt_qkv_min_k=1))
     prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 50))]
     sp = SamplingParams(greedy=True, max_new_tokens=12)
     a = _engine("llama-test", graphs=False).generate_ids(prompts, sp)
     e = _engine("llama-test", graphs=True)
     for _ in range(3):  # eager first use, capture, replay
         assert e.generate_ids(prompts, sp) == a
+
+
+def test_blaslt_oracle_stages_sharing_a_gpu_match_one_stage(monkeypatch):
+    """two pipeline stages on ONE GPU issue hipBLASLt GEMMs
+    concurrently from their own lane streams (graph-captured too).  Only
+    workspace-free algorithms are accepted, so nothing is shared: with every
+    library route forced on (decode QKV / gate_up from 1 row, prefill from 1
+    row) the 2-stage pipeline gives the 1-stage tokens."""
+    from llm_sharding_demo_amd.ops.hip import HipBackend
+
+    monkeypatch.setattr(HipBackend, "R", HipBackend.R.replace(
+        blaslt=1, blaslt_min_m=1, blaslt_resid_min_k=1, blaslt_gelu_min_m=1, blaslt_silu_min_m=1,
+        blaslt_silu_max_m=1 << 20, blaslt_qkv_min_m=1, blaslt_qkv_min_k=1))
+    prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 50)), [7] * 9]
+    sp = SamplingParams(greedy=True, max_new_tokens=10)
+    for model in ("llama-test", "gpt2-test"):
+        one = _engine(model, merge_prefill=False).generate_ids(prompts, sp, microbatches=2)
+        two = _engine(model, P=2).generate_ids(prompts, sp, microbatches=2)
+        assert one == two, model
 
 
 def test_pipeline_stages_bit_identical_on_one_gpu():

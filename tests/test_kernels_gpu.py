@@ -409,10 +409,11 @@ def D256(C, request):
     C.gemm_set_d256_slots(3)
 
 
-@pytest.mark.parametrize("M", [1, 100, 129, 200, 256])
+@pytest.mark.parametrize("M", [1, 100, 129, 200, 256, 300, 512, 700])
 @pytest.mark.parametrize("K,splits", [(64, 1), (192, 1), (192, 3), (640, 2), (640, 5), (1600, 3), (1600, 1)])
 def test_d256_gemm_epilogues(D256, CNT, M, K, splits):
-    """256-row decode kernel: every epilogue, row tails (1 to 256 rows), a
+    """256-row decode kernel: every epilogue, row tails (1 to 256 rows), rows
+    in several 256-row blocks (300 / 512 / 700: a partial last block), a
     partial last column tile, 1 to 25 k-steps (fewer than, equal to and more
     than the ring), split-K with the in-kernel last-arriver combine and the
     residual slabs folded by the norm; repeated launches reuse the re-armed
@@ -520,17 +521,19 @@ def _cache(slots, n_kv, S, hd):
 
 
 @pytest.mark.parametrize("rope", [False, True])
-@pytest.mark.parametrize("mode", ["decode1", "decode4", "tiled", "big", "d256", "d256s3"])
+@pytest.mark.parametrize("mode", ["decode1", "decode4", "tiled", "big", "d256", "d256s3", "d256rb"])
 def test_qkv_kv_append(C, CNT, rope, mode):
     from llm_sharding_demo_amd.ops.hip import rope_pair_permutation, rope_table
 
     nh, n_kv, hd, H = 4, 2, 64, 256
     qs, kvs = nh * hd, n_kv * hd
-    tiled = mode in ("tiled", "big", "d256", "d256s3")
-    splits = 4 if mode == "decode4" else (3 if mode == "d256s3" else 1)
+    tiled = mode in ("tiled", "big", "d256", "d256s3", "d256rb")
+    splits = 4 if mode == "decode4" else (3 if mode == "d256s3" else (2 if mode == "d256rb" else 1))
     # decode: 10 tokens of 2 sequences; tiled: 2 sequences of 150 tokens;
-    # d256: 200 decode-like rows (100 + 100) on the 256-row kernel (kind 2)
-    n0, n1 = (4, 6) if not tiled else ((100, 100) if mode.startswith("d256") else (150, 150))
+    # d256: 200 decode-like rows (100 + 100) on the 256-row kernel (kind 2);
+    # d256rb: 400 rows in two 256-row blocks, split-K combine
+    n0, n1 = (4, 6) if not tiled else ((100, 100) if mode in ("d256", "d256s3") else
+                                       ((200, 200) if mode == "d256rb" else (150, 150)))
     if mode.startswith("d256"):
         tiled = 2
     T, slots, S = n0 + n1, 3, 320
@@ -717,14 +720,17 @@ def test_linear_f32_segmax(C, CNT, M, N, K, kind, splits):
 
 @pytest.mark.parametrize("M,N,K", [(4096, 1600, 1600), (4100, 6400, 1600), (8192, 768, 3072)])
 def test_blaslt_prefill_projections(C, M, N, K):
-    """hipBLASLt prefill projections (csrc/blaslt.cpp): bf16 out with bias and
-    bias + GELU epilogues, and the fp32 residual accumulate (beta = 1, C = D =
-    x) -- against the fp32 reference; the library's GELU against GPT-2's
-    tanh-approximated gelu_new at bf16 resolution."""
+    """hipBLASLt prefill projections (csrc/blaslt.cpp, the opt-in A/B oracle):
+    bf16 out with bias and bias + GELU epilogues, and the fp32 residual
+    accumulate (beta = 1, C = D = x) -- against the fp32 reference; the
+    library's GELU against GPT-2's tanh-approximated gelu_new at bf16
+    resolution.  Only workspace-free algorithms are accepted: a shape the
+    library then declines is reported (None) and skipped here."""
     a, w, bias = bf(M, K, seed=95), bf(N, K, scale=0.05, seed=96), bf(N, scale=0.1, seed=97)
     y_ref = ref.linear(a, w, bias)
     y = C.blaslt_linear(a, w, bias, 0)
-    assert y is not None, "hipBLASLt has no algorithm for the prefill shape"
+    if y is None:
+        pytest.skip("hipBLASLt has no workspace-free algorithm for this shape")
     close(y, y_ref, 3e-2)
     close(C.blaslt_linear(a, w, bias, 1), ref.gelu_new(y_ref), 3e-2)
     close(C.blaslt_linear(a, w, None, 1), ref.gelu_new(ref.linear(a, w)), 3e-2)

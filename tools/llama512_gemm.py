@@ -56,9 +56,14 @@ def case(N, code, label, kind=True, splits=1, halves=False, big_min=160, tiled3=
 
 
 N_GU, N_QKV = 2 * 14336, 6144
-case(N_GU, 2, "gate_up p8 256x256 (default)")
-case(N_GU, 2, "gate_up tiled 128x128", big_min=1 << 30)
-case(N_GU, 2, "gate_up 2x d256-128 halves", kind=3, splits=1, halves=True)
-case(N_GU, 2, "gate_up 2x d256-128 halves s2", kind=3, splits=2, halves=True)
 case(N_QKV, 0, "qkv-shaped bf16 ring8 (default)")
-case(N_QKV, 0, "qkv-shaped bf16 tiled 128x128 (ring cap off)", tiled3=0)
+for kind, bn in ((2, 64), (3, 128)):
+    for S in (1, 2, 3, 4):
+        case(N_QKV, 0, f"qkv-shaped bf16 d256-{bn} row blocks s{S}", kind=kind, splits=S)
+case(N_GU, 2, "gate_up p8 256x256 (default)")
+for S in (1, 2):
+    case(N_GU, 2, f"gate_up d256-128 row blocks s{S}", kind=3, splits=S)
+N_O = 4096
+case(N_O, 0, "o-shaped bf16 d256-64 row blocks s2", kind=2, splits=2)
+case(N_O, 0, "o-shaped bf16 d256-64 row blocks s4", kind=2, splits=4)
+case(N_O, 0, "o-shaped bf16 d256-128 row blocks s4", kind=3, splits=4)
