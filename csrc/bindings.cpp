@@ -139,7 +139,7 @@ GemmParams base_params(const torch::Tensor& a, const torch::Tensor& w, int64_t t
   TORCH_CHECK(p.N % 16 == 0, "N must be a multiple of 16 (pad the weight), got ", p.N);
   TORCH_CHECK(tiled >= 0 && tiled <= 3, "GEMM kind must be 0 (split-K), 1 (tiled), 2 / 3 (256-row), got ", tiled);
   if (tiled >= 2)
-    TORCH_CHECK(p.M >= 1 && p.M <= 256, "256-row decode GEMM needs 1 <= M <= 256, got ", p.M);
+    TORCH_CHECK(p.M >= 1 && p.M <= 1024, "256-row-block decode GEMM needs 1 <= M <= 1024, got ", p.M);
   if (tiled) {
     TORCH_CHECK(p.K % 64 == 0, "tiled GEMM needs K % 64 == 0, got ", p.K);
   } else {

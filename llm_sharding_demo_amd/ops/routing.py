@@ -88,6 +88,12 @@ class Routing:
     d256_min_k: int = 4096
     d256_slots: int = 3
     d256_target: int = 192
+    # ... and over 256-row blocks up to d256_rb_max_m rows for long-K GEMMs at
+    # most d256_rb_max_n wide: Llama-3 8B QKV at 512 rows 54.6 (8-wave ring)
+    # -> 45.2 us (128-wide tiles, 2 K splits; the 28672-wide gate_up stays on
+    # the 256x256 kernel: 120 vs 145 us; profiles/r6_llama512_gemm.log)
+    d256_rb_max_m: int = 512
+    d256_rb_max_n: int = 8192
     # the 256x256 pipelined kernel (gemm_p8) once a tiled launch has this
     # many 256x256 tiles; the 128x128 kernels below (launch_tiled in gemm.hip)
     big_min_blocks: int = 160
@@ -136,7 +142,13 @@ class Routing:
     def d256_bn(self, M: int, N: int, K: int) -> int:
         """Tile columns when this GEMM runs on gemm_d256_kernel, else 0
         (mirrors d256_bn() in gemm.hip)."""
-        if not self.d256 or not (128 < M <= 256) or K % 64 or N > 32768 or not self.tiled(M, N):
+        if not self.d256 or K % 64 or N > 32768 or not self.tiled(M, N):
+            return 0
+        if 256 < M <= self.d256_rb_max_m:  # several 256-row blocks (auto only)
+            if self.d256 != 1 or K < self.d256_min_k or N > self.d256_rb_max_n:
+                return 0
+            return 128 if N % 128 == 0 else 64
+        if not (128 < M <= 256):
             return 0
         if self.d256 == 1:  # auto: long-K GEMMs; 128-wide tiles when they alone fill the chip
             if K < self.d256_min_k:
@@ -149,8 +161,8 @@ class Routing:
         return 3 if bn == 128 else 2
 
     @staticmethod
-    def d256_splits(N: int, K: int, bn: int, target: int) -> int:
-        tiles = math.ceil(N / bn)
+    def d256_splits(N: int, K: int, bn: int, target: int, M: int = 256) -> int:
+        tiles = math.ceil(N / bn) * math.ceil(M / 256)  # column tiles x 256-row blocks
         return max(1, min(round(target / tiles), K // 64 // 2 or 1, 16))
 
     def sk_splits(self, M: int, N: int, K: int, lanes: int = 1, nw: int = 1) -> int:
@@ -164,7 +176,7 @@ class Routing:
         gate_up, lm_head below vocab width)."""
         bn = self.d256_bn(M, N, K)
         if bn:
-            return self.d256_kind(bn), self.d256_splits(N, K, bn, self.d256_target)
+            return self.d256_kind(bn), self.d256_splits(N, K, bn, self.d256_target, M)
         if self.tiled(M, N) or (K <= self.tiled_short_k and M <= self.sk_max_m and K % 64 == 0):
             return True, 1
         return False, self.sk_splits(M, N, K, lanes, nw)
