@@ -165,7 +165,7 @@ def main() -> int:
     barrier()
     sync()
     t0 = time.perf_counter()
-    step_ms, prefill_ms, max_step = [], [], []
+    step_ms, prefill_ms, max_step, decode_sum = [], [], [], []
     for _ in range(args.steps):
         session(True)
         if rank == 0 and eng.last_session is not None:
@@ -173,6 +173,7 @@ def main() -> int:
             step_ms += ls.step_times_ms
             prefill_ms.append(ls.prefill_ms)
             max_step.append(max(ls.step_times_ms, default=0.0))
+            decode_sum.append(sum(ls.step_times_ms))
     sync()
     barrier()
     sync()
@@ -213,6 +214,10 @@ def main() -> int:
             # and the slowest decode step (graphs are cached across sessions)
             "prefill_ms": round(statistics.mean(prefill_ms), 3) if prefill_ms else None,
             "max_decode_step_ms": round(statistics.mean(max_step), 3) if max_step else None,
+            # the rest of a step on the host clock: session setup / drain and the
+            # last decode step (the stage-0 events time the steps between starts)
+            "session_other_ms": (round(ms_per_step - statistics.mean(prefill_ms) - statistics.mean(decode_sum), 3)
+                                 if prefill_ms and decode_sum else None),
             "config": {"model": args.model, "global_batch": B, "seq_len": args.prompt + args.gen,
                        "prompt_len": args.prompt, "gen_tokens": args.gen, "microbatches": M,
                        "prefill_chunk": chunk,

@@ -353,6 +353,15 @@ class RcclTransport(_DistTransport):
         except Exception as e:  # noqa: BLE001 - every rank must learn the outcome
             err = f"rank {self.grank}: {type(e).__name__}: {e}"
         self.agree(err, "native RCCL unavailable")
+        # the bounded init runs on a helper thread, and the current HIP device
+        # is per thread: bind it to this rank's GPU there, or every rank's
+        # communicators would land on device 0
+        dev_idx = torch.cuda.current_device()
+
+        def comm_init(me: int, uid: bytes) -> int:
+            torch.cuda.set_device(dev_idx)
+            return self.C.rccl_comm_init(2, me, uid)
+
         try:
             for name in self.groups:
                 members = self._members(name)
@@ -366,7 +375,7 @@ class RcclTransport(_DistTransport):
                     uid = self.broadcast_object(uid, src=members[0])
                     if self.grank in members and err is None and uid is not None:
                         me = members.index(self.grank)
-                        h, err = _bounded(lambda: self.C.rccl_comm_init(2, me, uid), init_s,
+                        h, err = _bounded(lambda: comm_init(me, uid), init_s,
                                           f"rank {self.grank}: ncclCommInitRank {name}/lane{lane}")
                         if h:
                             self.comms[(name, lane)] = (h, me)

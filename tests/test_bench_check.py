@@ -118,3 +118,18 @@ def test_devloop_bench_reports_token_check(world):
                             "--transport", "devloop"], env_extra={"LSD_LOOP_RING_MB": "16"})
     assert r.returncode == 0 and out is not None, (r.stdout[-2000:], r.stderr[-3000:])
     assert out["pipeline_matches_1gpu"] is True and out["transport"] == "devloop", out
+
+
+def test_bounded_reports_a_hang_and_an_error():
+    """The bring-up helper for blocking communicator inits: a call that does
+    not return by the deadline and a call that raises both come back as an
+    error string (the caller agrees on it with every rank), never a hang."""
+    import time
+
+    from llm_sharding_demo_amd.parallel.comm import _bounded
+
+    r, err = _bounded(lambda: time.sleep(5), 0.2, "stuck init")
+    assert r is None and "no result after" in err
+    r, err = _bounded(lambda: 1 // 0, 5.0, "bad init")
+    assert r is None and "ZeroDivisionError" in err
+    assert _bounded(lambda: 7, 5.0, "ok") == (7, None)

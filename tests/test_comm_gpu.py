@@ -95,3 +95,32 @@ def test_rccl_rejects_bad_input(comm):
         C.rccl_send(h, torch.zeros(4), 0)  # host tensor
     with pytest.raises((ValueError, RuntimeError)):
         C.rccl_comm_init(1, 0, b"short")
+
+
+def test_rccl_comm_init_on_a_helper_thread():
+    """RcclTransport runs each blocking ncclCommInitRank on a helper thread
+    with a deadline (parallel/comm.py _bounded); the HIP device is per
+    thread, so the helper binds the rank's GPU first.  The communicator it
+    makes is used from the calling thread."""
+    from llm_sharding_demo_amd.ops.hip import _load
+    from llm_sharding_demo_amd.parallel.comm import _bounded
+
+    C = _load()
+    dev = torch.cuda.current_device()
+    uid = C.rccl_unique_id()
+
+    def init():
+        torch.cuda.set_device(dev)
+        return C.rccl_comm_init(1, 0, uid)
+
+    h, err = _bounded(init, 60.0, "init")
+    assert err is None and h
+    src = torch.arange(1000, device="cuda", dtype=torch.float32)
+    dst = torch.zeros_like(src)
+    C.rccl_group_start()
+    C.rccl_send(h, src, 0)
+    C.rccl_recv(h, dst, 0)
+    C.rccl_group_end()
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src)
+    C.rccl_comm_destroy(h)
