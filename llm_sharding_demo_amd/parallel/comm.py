@@ -345,18 +345,19 @@ class RcclTransport(_DistTransport):
         self._issue = threading.Condition()
         self._inflight = 0
         err = None
+        dev_idx = 0
         try:
             from ..ops.hip import _load
 
             self.C = _load()
             self.C.rccl_version()  # resolves librccl and its symbols
+            # the bounded init runs on a helper thread, and the current HIP
+            # device is per thread: bind it to this rank's GPU there, or every
+            # rank's communicators would land on device 0
+            dev_idx = torch.cuda.current_device()
         except Exception as e:  # noqa: BLE001 - every rank must learn the outcome
             err = f"rank {self.grank}: {type(e).__name__}: {e}"
         self.agree(err, "native RCCL unavailable")
-        # the bounded init runs on a helper thread, and the current HIP device
-        # is per thread: bind it to this rank's GPU there, or every rank's
-        # communicators would land on device 0
-        dev_idx = torch.cuda.current_device()
 
         def comm_init(me: int, uid: bytes) -> int:
             torch.cuda.set_device(dev_idx)

@@ -133,3 +133,16 @@ def test_bounded_reports_a_hang_and_an_error():
     r, err = _bounded(lambda: 1 // 0, 5.0, "bad init")
     assert r is None and "ZeroDivisionError" in err
     assert _bounded(lambda: 7, 5.0, "ok") == (7, None)
+
+
+def test_native_rccl_unavailable_falls_back_on_every_rank():
+    """The real RcclTransport bring-up on a box without GPUs: every rank fails
+    its first step (no HIP device), the failure is agreed over the gloo
+    control group, and both ranks bring up the next transport of the chain
+    in process; the run reports why and still matches one stage."""
+    cpu = [a for a in CPU if a != "gloo"]
+    cpu[cpu.index("--transport") + 1:cpu.index("--transport") + 1] = ["rccl,gloo"]
+    r, out = _bench(2, cpu)
+    assert r.returncode == 0 and out is not None, r.stderr[-3000:]
+    assert out["transport"] == "gloo" and "native RCCL unavailable" in (out["transport_fallback"] or ""), out
+    assert out["pipeline_matches_1gpu"] is True, out
