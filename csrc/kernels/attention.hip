@@ -739,8 +739,9 @@ static int g_attn_large_waves64 = 4, g_attn_large_waves128 = 4;
 static int g_attn_mfma_min = 256;
 extern "C" void lsd_attn_set_mfma_min(int v) { g_attn_mfma_min = v; }
 extern "C" void lsd_attn_set_large_waves(int hd, int v) {
-  if (hd == 64) g_attn_large_waves64 = v == 8 ? 8 : 4;
-  else g_attn_large_waves128 = v == 8 ? 8 : 4;
+  v = (v == 8 || v == 42 || v == 2) ? v : 4;
+  if (hd == 64) g_attn_large_waves64 = v;
+  else g_attn_large_waves128 = v;
 }
 
 static hipError_t attn_decode_combine(const float* part_o, const float* part_ml, bf16* out, long ldo,
@@ -781,8 +782,10 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
     LSD_DEC_MFMA(8)
 #undef LSD_DEC_MFMA
   }
-  const int sw = (long)gx * splits <= 128 ? g_attn_small_waves
-                                           : ((hd == 64 ? g_attn_large_waves64 : g_attn_large_waves128) == 8 ? 8 : 0);
+  // full batches: 4 waves (unroll 4) by default; 8 waves, 4 waves with
+  // unroll 2 (42) and 2 waves (2) for A/B (lsd_attn_set_large_waves)
+  const int lw = hd == 64 ? g_attn_large_waves64 : g_attn_large_waves128;
+  const int sw = (long)gx * splits <= 128 ? g_attn_small_waves : (lw == 8 || lw == 42 || lw == 2 ? lw : 0);
   dim3 grid(gx, splits);
 #define LSD_DEC(HDV, GV)                                                                        \
   if (hd == HDV && G == GV) {                                                                   \
@@ -792,6 +795,14 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
                          splits, scale_log2, n_items);                                          \
     else if (sw == 8)                                                                           \
       hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 4, 8>), grid, dim3(512), 0, st, q, ldq,   \
+                         kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq,     \
+                         splits, scale_log2, n_items);                                          \
+    else if (sw == 42)                                                                          \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 2, 4>), grid, dim3(256), 0, st, q, ldq,   \
+                         kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq,     \
+                         splits, scale_log2, n_items);                                          \
+    else if (sw == 2)                                                                           \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 4, 2>), grid, dim3(128), 0, st, q, ldq,   \
                          kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq,     \
                          splits, scale_log2, n_items);                                          \
     else                                                                                        \

@@ -586,6 +586,19 @@ def test_attention_decode(C, hd, nh, n_kv, splits, max_wg, B, small_waves):
         C.attn_set_small_waves(8)
 
 
+@pytest.mark.parametrize("hd,nh,n_kv", [(64, 12, 12), (128, 8, 2)])
+@pytest.mark.parametrize("lw", [8, 42, 2])
+def test_attention_decode_full_batch_blocks(C, hd, nh, n_kv, lw):
+    """Full-batch block shapes of the VALU decode kernel (A/B variants of the
+    4-wave default): 8 waves, 4 waves with 2 keys per wave in flight, 2 waves."""
+    C.attn_set_large_waves(hd, lw)
+    try:
+        _attention_decode_case(C, hd, nh, n_kv, 1, 70)
+        _attention_decode_case(C, hd, nh, n_kv, 3, 70)
+    finally:
+        C.attn_set_large_waves(hd, 4)
+
+
 def _attention_decode_case(C, hd, nh, n_kv, splits, B=5):
     slots, S = max(6, B), 300
     kc, vc = bf(slots, n_kv, S, hd, seed=16), bf(slots, n_kv, S, hd, seed=17)
