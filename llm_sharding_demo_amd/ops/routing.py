@@ -45,7 +45,10 @@ class Routing:
     attn_mfma_split_below: int = 1024
     attn_mfma_waves: int = 1024
     attn_small_waves: int = 8  # waves per small-batch VALU attention block
-    attn_large_waves: int = 4  # full-batch block: 8 waves 10 % slower (r4_attn_large_waves.log)
+    # full-batch block: 4 waves; 8 waves 10 % slower (r4_attn_large_waves.log); 42 = 4 waves with 2
+    # keys per wave in flight and 2 = 2-wave blocks: faster alone at <= 192 keys, slower in the
+    # two-lane bench (XL p50 8.44 -> 8.58-8.63 ms; r6_attn_ab.log)
+    attn_large_waves: int = 4
     attn_max_wg: int = 0       # cap the attention grid (A/B; 0 = none)
     # -- decode GEMMs ------------------------------------------------------
     # split-K (last-arriver) kernel up to sk_max_m rows; tiled above
