@@ -103,7 +103,7 @@ def main() -> int:
     import torch
 
     from llm_sharding_demo_amd.config import EngineConfig, SamplingParams
-    from llm_sharding_demo_amd.runtime.engine import Engine
+    from llm_sharding_demo_amd.runtime.engine import Engine, freeze_gc
 
     N = args.gpus
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -161,9 +161,14 @@ def main() -> int:
 
     for _ in range(args.warmup):
         session(False)
+    if os.environ.get("BENCH_GC_FREEZE", "1") == "1":
+        freeze_gc()  # as the server does after start-up (engine.freeze_gc)
     sync()
     barrier()
     sync()
+    if getattr(eng, "_phases", None):
+        eng._phases.clear()
+        eng._hostprof[:] = [0.0, 0.0, 0.0, 0, 0, 0.0, 0.0, 0]
     t0 = time.perf_counter()
     step_ms, prefill_ms, max_step, decode_sum = [], [], [], []
     for _ in range(args.steps):
@@ -260,6 +265,8 @@ def main() -> int:
                   f"({hp[1] / max(hp[4], 1) * 1e6:.1f} us per item; issuing-thread CPU "
                   f"{hp[5] / max(hp[4], 1) * 1e6:.1f} us per item), readout wait "
                   f"{hp[2] / hp[3] * 1e6:.1f} us over {hp[3]} steps", file=sys.stderr)
+            print("host per session (ms): " + ", ".join(f"{k} {v * 1e3 / args.steps:.2f}"
+                                                        for k, v in eng._phases.items()), file=sys.stderr)
     if N > 1:
         if rank == 0:
             eng.shutdown()  # stop the followers, barrier, tear the groups down in order

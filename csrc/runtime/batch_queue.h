@@ -48,6 +48,21 @@ class BatchQueue {
     return true;
   }
 
+  // push() of a whole batch under one lock / one wake-up: false (nothing
+  // queued) when closed.
+  bool push_many(const std::vector<int64_t>& ids, const std::vector<int>& max_new) {
+    if (ids.size() != max_new.size()) throw std::invalid_argument("push_many: length mismatch");
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (closed_) return false;
+      for (size_t i = 0; i < ids.size(); ++i)
+        q_.push_back(Item{ids[i], max_new[i] < 1 ? 1 : max_new[i]});
+      pushed_ += (int64_t)ids.size();
+    }
+    cv_.notify_all();
+    return true;
+  }
+
   // One scheduling decision.  Empty result == closed (nothing more will come
   // out; remaining ids are returned by drain()).
   std::vector<std::vector<int64_t>> next_groups(double window_s) {

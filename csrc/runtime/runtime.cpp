@@ -84,6 +84,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def(py::init<int, double>(), py::arg("max_batch"), py::arg("length_ratio") = 4.0)
       .def("push", &BatchQueue::push, py::arg("id"), py::arg("max_new_tokens"),
            py::call_guard<py::gil_scoped_release>())
+      .def("push_many", &BatchQueue::push_many, py::arg("ids"), py::arg("max_new_tokens"))
       .def("next_groups", &BatchQueue::next_groups, py::arg("window_s"),
            py::call_guard<py::gil_scoped_release>())
       .def("try_pop", &BatchQueue::try_pop, py::arg("k"))
@@ -104,6 +105,8 @@ PYBIND11_MODULE(_runtime, m) {
            py::keep_alive<1, 8>())  // the pools outlive the core
       .def("add", &SchedCore::add, py::arg("sid"), py::arg("prompt_len"), py::arg("want"),
            py::arg("stop_at_eos"))
+      .def("add_many", &SchedCore::add_many, py::arg("sids"), py::arg("prompt_lens"),
+           py::arg("wants"), py::arg("stops"))
       .def("has_work", &SchedCore::has_work)
       .def("plan", [](SchedCore& c, int64_t step) {
              std::vector<int64_t> admitted;

@@ -104,6 +104,17 @@ class SchedCore {
     waiting_.push_back(sid);
   }
 
+  // add() of a whole batch (one call from the scheduler's bulk admission)
+  void add_many(const std::vector<int64_t>& sids, const std::vector<int>& prompt_lens,
+                const std::vector<int>& wants, const std::vector<bool>& stops) {
+    const size_t n = sids.size();
+    if (prompt_lens.size() != n || wants.size() != n || stops.size() != n)
+      throw std::invalid_argument("add_many: length mismatch");
+    for (size_t i = 0; i < n; ++i)
+      if (prompt_lens[i] <= 0) throw std::invalid_argument("empty prompt");
+    for (size_t i = 0; i < n; ++i) add(sids[i], prompt_lens[i], wants[i], stops[i]);
+  }
+
   bool has_work() const {
     if (!waiting_.empty()) return true;
     for (const auto& rep : groups_)

@@ -87,9 +87,10 @@ def main(argv=None) -> int:
     elif cfg.transport == "http":  # reference-style coordinator over remote shards
         app = create_app(cfg)
     else:
-        from .runtime.engine import build_engine
+        from .runtime.engine import build_engine, freeze_gc
 
         engine = build_engine(cfg)
+        freeze_gc()
         if engine.mode == "dist" and engine.rank != 0:
             engine.worker_loop()
             return 0

@@ -30,6 +30,7 @@ import queue
 import random
 import statistics
 import threading
+import gc
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
@@ -120,6 +121,8 @@ class Engine(racecheck.Shared):
         # LSD_HOST_PROFILE=1: host seconds in (plan, issue, readout wait), steps,
         # items, issuing-thread CPU, plan-send seconds, plan bytes sent
         self._hostprof = [0.0, 0.0, 0.0, 0, 0, 0.0, 0.0, 0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
+        # LSD_HOST_PROFILE: host-clock seconds per session phase, summed over sessions
+        self._phases: Optional[Dict[str, float]] = {} if self._hostprof is not None else None
         self.kv_slots = 0
         self._stall_after: Optional[int] = None  # test hook, see _test_stall
         # dist mode: the data plane in use and why the preferred one was left
@@ -384,6 +387,8 @@ class Engine(racecheck.Shared):
                      record_timing: bool = False) -> List[List[int]]:
         """Generate continuations for token-id prompts (generated ids only).
         Runs the driver loop on this thread unless the serving loop is up."""
+        ph = self._phases
+        tp = time.monotonic() if ph is not None else 0.0
         if isinstance(params, SamplingParams):
             params = [params] * len(prompts)
         for p, sp in zip(prompts, params):
@@ -392,12 +397,24 @@ class Engine(racecheck.Shared):
             raise RuntimeError(f"engine unhealthy: {self.last_error}")
         if microbatches and microbatches != self.M and self.loop_thread is None:
             self.set_groups(microbatches)
-        reqs = [self.scheduler.submit(p, sp) for p, sp in zip(prompts, params)]
+        reqs = self.scheduler.submit_many(prompts, params)
         if self.loop_thread is not None:
             return [r.wait() for r in reqs]
+        if ph is not None:
+            self._phase("validate+submit", tp)
         with self._lock:
             self._drive(lambda: all(r.done for r in reqs), timing=record_timing)
-        return [r.wait(0) for r in reqs]
+        tp = time.monotonic() if ph is not None else 0.0
+        out = [r.wait(0) for r in reqs]
+        if ph is not None:
+            self._phase("collect", tp)
+        return out
+
+    def _phase(self, name: str, t0: float) -> float:
+        """LSD_HOST_PROFILE: add the host time since t0 to session phase `name`."""
+        t = time.monotonic()
+        self._phases[name] = self._phases.get(name, 0.0) + (t - t0)
+        return t
 
     def set_groups(self, M: int) -> None:
         """Re-shape the microbatch groups (only between sessions)."""
@@ -440,6 +457,8 @@ class Engine(racecheck.Shared):
             self._start_stats()
         lag = self.P + 2  # steps the host may run ahead of the GPU readouts
         hp = self._hostprof
+        ph = self._phases
+        tp = time.monotonic()
         ran = False
         try:
             cur = sch.build_step()
@@ -447,6 +466,8 @@ class Engine(racecheck.Shared):
                 ran = True
                 self._send_plans(cur)
                 w0.begin_session()
+            if ph is not None:
+                tp = self._phase("first plan", tp)
             while cur is not None:
                 self._check_followers()
                 if not self.healthy:
@@ -476,6 +497,8 @@ class Engine(racecheck.Shared):
                 cur = nxt
             if ran:
                 w0.end_session()
+            if ph is not None:
+                tp = self._phase("step loop", tp)
             # everything issued: wait for the outstanding readouts
             while sch.readouts or not until():
                 if sch.readouts:
@@ -487,6 +510,8 @@ class Engine(racecheck.Shared):
                         raise RuntimeError(self.last_error)
                     time.sleep(0.0005)
                     sch.poll()
+            if ph is not None:
+                tp = self._phase("drain", tp)
         except BaseException as e:
             self.healthy = False
             self.last_error = f"{type(e).__name__}: {e}"
@@ -496,6 +521,8 @@ class Engine(racecheck.Shared):
             self._round(None)
         if timing and ran:
             self._finish_stats()
+            if ph is not None:
+                self._phase("stats", tp)
 
     def _check_followers(self) -> None:
         err = getattr(self, "_follow_err", None)
@@ -814,6 +841,18 @@ def _make_slot_allocator(n: int):
     if mod is not None and os.environ.get("LSD_PY_RUNTIME", "0") != "1":
         return mod.SlotAllocator(n)
     return SlotAllocator(n)
+
+
+def freeze_gc() -> None:
+    """Move every object alive now (model, torch / HIP wrappers, captured
+    graphs) out of the cyclic collector's reach (gc.freeze): a 4096-request
+    session allocates enough small objects to trigger full collections, and
+    each one walked the whole engine (a second session's submit took
+    194 ms instead of 61 ms on the CPU, profiles/r6_session_host.log).
+    Called once the engine is built and warmed up; objects created later are
+    collected as usual."""
+    gc.collect()
+    gc.freeze()
 
 
 def build_engine(cfg: EngineConfig, **kw) -> Engine:

@@ -50,8 +50,16 @@ class RequestTimeout(RuntimeError):
     pass
 
 
-@dataclass
+_FINISH = threading.Lock()  # orders Request.finish against a waiter creating its event
+
+
+@dataclass(eq=False)
 class Request:
+    """One generation request.  Light on purpose: a 4096-sequence session
+    creates 4096 of these on the submitting thread, so the completion event
+    is made only when someone actually blocks in wait() before the request
+    finishes (a threading.Event per request was ~6 us of the ~14 us
+    submit cost, profiles/r6_session_host.log)."""
     prompt_ids: List[int]
     params: SamplingParams
     t_submit: float = field(default_factory=time.monotonic)
@@ -60,23 +68,33 @@ class Request:
     t_done: float = 0.0
     output: Optional[List[int]] = None
     error: Optional[BaseException] = None
-    _done: threading.Event = field(default_factory=threading.Event)
+    _flag: bool = False
+    _ev: Optional[threading.Event] = None
 
     def wait(self, timeout: Optional[float] = None) -> List[int]:
-        if not self._done.wait(timeout):
-            raise RequestTimeout(f"request not finished after {timeout} s")
+        if not self._flag:
+            with _FINISH:
+                if not self._flag and self._ev is None:
+                    self._ev = threading.Event()
+                ev = self._ev
+            if ev is not None and not ev.wait(timeout):
+                raise RequestTimeout(f"request not finished after {timeout} s")
         if self.error is not None:
             raise self.error
         return self.output
 
     @property
     def done(self) -> bool:
-        return self._done.is_set()
+        return self._flag
 
     def finish(self, output=None, error=None) -> None:
         self.output, self.error = output, error
         self.t_done = time.monotonic()
-        self._done.set()
+        with _FINISH:
+            self._flag = True
+            ev = self._ev
+        if ev is not None:
+            ev.set()
 
 
 class PyBatchQueue(racecheck.Shared):
@@ -101,6 +119,17 @@ class PyBatchQueue(racecheck.Shared):
             self._q.append((id, max(1, max_new_tokens)))
             self.pushed += 1
             self._cv.notify()
+            return True
+
+    def push_many(self, ids: List[int], max_new_tokens: List[int]) -> bool:
+        if len(ids) != len(max_new_tokens):
+            raise ValueError("push_many: length mismatch")
+        with self._cv:
+            if self._closed:
+                return False
+            self._q.extend((i, max(1, n)) for i, n in zip(ids, max_new_tokens))
+            self.pushed += len(ids)
+            self._cv.notify_all()
             return True
 
     def next_groups(self, window_s: float) -> List[List[int]]:
@@ -251,6 +280,14 @@ class PySchedCore:
             raise ValueError("empty prompt")
         self.seqs[sid] = _Seq(prompt_len, want, stop_at_eos)
         self.waiting.append(sid)
+
+    def add_many(self, sids, prompt_lens, wants, stops) -> None:
+        if not len(sids) == len(prompt_lens) == len(wants) == len(stops):
+            raise ValueError("add_many: length mismatch")
+        if any(n <= 0 for n in prompt_lens):
+            raise ValueError("empty prompt")
+        for a in zip(sids, prompt_lens, wants, stops):
+            self.add(*a)
 
     def has_work(self) -> bool:
         if self.waiting:
@@ -458,7 +495,7 @@ def make_sched_core(replicas: int, groups: int, cap: int, prefill_budget: int, c
 class _Meta:
     req: Request
     seed: int
-    tokens: List[int] = field(default_factory=list)
+    samp: tuple = ()    # (temperature, top_k, greedy, seed): the chunk / row sampling fields
     done: bool = False  # finished by this scheduler (plain flag: the readout loop's hot path)
 
 
@@ -506,20 +543,53 @@ class Scheduler(racecheck.Shared):
             raise RuntimeError("scheduler is closed")
         return req
 
+    def submit_many(self, prompts: List[List[int]], params: List[SamplingParams]) -> List[Request]:
+        """submit() for a whole batch: one pass under the pending-map lock
+        (a 4096-sequence bench session submits everything at once)."""
+        now = time.monotonic()
+        # a list whose first token is a Python int is taken as a list of ints
+        # and only copied (list(map(int, .)) per 64-token prompt was ~4 us,
+        # 17 ms of a 4096-prompt session); anything else is converted
+        reqs = [Request(list(p) if type(p) is list and p and type(p[0]) is int else list(map(int, p)), sp, now)
+                for p, sp in zip(prompts, params)]
+        live = []
+        for req in reqs:
+            if req.params.max_new_tokens == 0:
+                req.finish([])
+            else:
+                live.append((next(self._ids), req))
+        with self._plock:
+            racecheck.note(self, "_pending")
+            self._pending.update(live)
+        if not self.queue.push_many([rid for rid, _ in live], [r.params.max_new_tokens for _, r in live]):
+            with self._plock:
+                racecheck.note(self, "_pending")
+                for rid, _ in live:
+                    self._pending.pop(rid, None)
+            raise RuntimeError("scheduler is closed")
+        return reqs
+
     @property
     def queue_depth(self) -> int:
         return self.queue.depth + self.core.n_waiting
 
     def _take_new(self) -> None:
         ids = self.queue.try_pop(1 << 20)
+        if not ids:
+            return
         with self._plock:
             racecheck.note(self, "_pending")
-            reqs = [(i, self._pending.pop(i)) for i in ids]
-        for i, req in reqs:
+            reqs = [self._pending.pop(i) for i in ids]
+        meta, rng = self.meta, self._rng
+        lens, wants, stops = [], [], []
+        for i, req in zip(ids, reqs):
             p = req.params
-            seed = p.seed if p.seed is not None else self._rng.getrandbits(62)
-            self.meta[i] = _Meta(req, seed)
-            self.core.add(i, len(req.prompt_ids), p.max_new_tokens, bool(p.stop_at_eos))
+            seed = p.seed if p.seed is not None else rng.getrandbits(62)
+            meta[i] = _Meta(req, seed, (p.temperature, p.top_k, p.greedy, seed))
+            lens.append(len(req.prompt_ids))
+            wants.append(p.max_new_tokens)
+            stops.append(bool(p.stop_at_eos))
+        self.core.add_many(ids, lens, wants, stops)
 
     def has_work(self) -> bool:
         """Anything left to plan OR to read back: token readouts still queued
@@ -554,18 +624,11 @@ class Scheduler(racecheck.Shared):
         g, ret, n, b, ctxb, changed, chunks, rows = go
         gp = GroupPlan(g, ret=ret, n=n, b=b, ctxb=ctxb)
         meta = self.meta
-        for sid, slot, start, ln, final in chunks:
-            m = meta[sid]
-            p = m.req.params
-            gp.chunks.append(Chunk(sid, slot, start, m.req.prompt_ids[start:start + ln], final,
-                                   p.temperature, p.top_k, p.greedy, m.seed))
+        gp.chunks = [Chunk(sid, slot, start, m.req.prompt_ids[start:start + ln], final, *m.samp)
+                     for sid, slot, start, ln, final in chunks for m in (meta[sid],)]
         if changed:
-            out = []
-            for sid, slot, pos, sstep, src in rows:
-                m = meta[sid]
-                p = m.req.params
-                out.append(Row(sid, slot, pos, p.temperature, p.top_k, p.greedy, m.seed, sstep, src))
-            gp.rows = out
+            gp.rows = [Row(sid, slot, pos, *meta[sid].samp, sstep, src)
+                       for sid, slot, pos, sstep, src in rows]
         return gp
 
     # -- token readout -----------------------------------------------------------

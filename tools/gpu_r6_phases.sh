@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 6: where a session's host time goes outside the timed GPU steps (LSD_HOST_PROFILE phases)
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+L=gpurun_out/r6_phases.log; : > $L
+run() {
+  echo "== $*" >> $L
+  LSD_HOST_PROFILE=1 timeout -k 10 400 python -u bench.py --steps 2 --warmup 1 "$@" > gpurun_out/_r.out 2> gpurun_out/_r.err || { tail -20 gpurun_out/_r.err >> $L; exit 1; }
+  cat gpurun_out/_r.out >> $L; grep "^host per" gpurun_out/_r.err >> $L
+}
+run --model gpt2 --batch 4096 --microbatches 16 --prompt 64 --gen 64
+run --model gpt2 --batch 4096 --microbatches 16 --prompt 64 --gen 64 --loopback-stages 8
+run
