@@ -63,6 +63,7 @@ hipError_t lsd_attn_oproj(const bf16* q, long ldq, const bf16* kc, const bf16* v
 int lsd_gemv_ok(int M, int K, int epi, int norm);
 void lsd_gemv_set_nt(int v);
 hipError_t lsd_gemv(const lsd::GemvParams* p, int epi, int norm, hipStream_t st);
+hipError_t lsd_apply_rows(const int64_t* args, int b, hipStream_t st);
 hipError_t lsd_silu_mul(const lsd_bf16_t* y, long ldy, lsd_bf16_t* out, long ldo, int M, int F, hipStream_t st);
 hipError_t lsd_qkv_post(const float* y, long ldy, const lsd_bf16_t* bias, const int* tslot, const int* tpos,
                         const float* rope, lsd_bf16_t* q, lsd_bf16_t* kc, lsd_bf16_t* vc, int M, int q_size,
@@ -680,6 +681,14 @@ torch::Tensor qkv_post(torch::Tensor y, c10::optional<torch::Tensor> bias, torch
   return q;
 }
 
+// Composition change of a decode group: args = the host int64 record of
+// elementwise.hip lsd_apply_rows (CPU tensor), on the current stream.
+void apply_rows(torch::Tensor args, int64_t b) {
+  TORCH_CHECK(args.device().is_cpu() && args.scalar_type() == torch::kInt64 && args.is_contiguous() &&
+                  args.numel() == 12, "apply_rows: args must be a contiguous CPU int64[12] record");
+  check_hip(lsd_apply_rows(args.data_ptr<int64_t>(), (int)b, cur_stream()), "apply_rows");
+}
+
 torch::Tensor silu_mul(torch::Tensor y) {
   need(y, torch::kBFloat16, "y");
   TORCH_CHECK(y.dim() == 2 && y.stride(1) == 1 && y.size(1) % 32 == 0, "silu_mul: y [M, 2F], 2F % 32 == 0");
@@ -740,6 +749,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pos") = py::none(), py::arg("segmax") = py::none());
   m.def("gemv", &gemv);
   m.def("silu_mul", &silu_mul);
+  m.def("apply_rows", &apply_rows, py::arg("args"), py::arg("b"));
   m.def("qkv_post", &qkv_post);
   // GEMV weight stream with non-temporal loads (A/B knob, LSD_GEMV_NT)
   m.def("gemv_set_nt", [](int64_t v) { lsd_gemv_set_nt((int)v); });

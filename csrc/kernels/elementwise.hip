@@ -103,3 +103,69 @@ extern "C" hipError_t lsd_qkv_post(const float* y, long ldy, const bf16* bias, c
                      rope, q, kc, vc, M, q_size, kv_size, hd, n_kv, max_seq);
   return hipGetLastError();
 }
+
+namespace lsd {
+
+// Composition change of a decode group (runtime/plan.py Row; the host side is
+// parallel/pipeline.py _apply_rows): the new rows' state arrives as ONE packed
+// int32 buffer (one host-to-device copy) laid out by the group capacity `cap`
+//   [0, 2 cap)      int64 sampler seeds        [2 cap, 4 cap)  int64 sampler steps
+//   [4 cap]         n (live rows)              then, from f = 4 cap + 1:
+//   f[0, cap) KV slots  f[cap, 2 cap) positions  f[2 cap, 3 cap) temperatures (fp32 bits)
+//   f[3 cap, 4 cap) top-k  f[4 cap, 5 cap) greedy  f[5 cap, 6 cap) stage 0's gather index
+// and this kernel scatters it into the group's row-state vectors: rows [0, n)
+// live, pad rows [n, b) idle on the scratch slot (position 0, inactive,
+// temperature 1, top-k 1, greedy, seed 0, step 0, gather index 0).  Stage 0
+// also gathers the rows' input tokens out of the previous token-return vector
+// in place (tin[i] = tin[src[i]], staged through LDS: a source may be a row
+// this same launch overwrites).  One workgroup: b <= 16384 (64 KB of LDS).
+// Replaces ~10 copy / index_select launches per changed item and lets the
+// native executor (csrc/stage_exec.cpp) issue composition-change items.
+__global__ __launch_bounds__(1024) void apply_rows_kernel(const int* __restrict__ buf, int b, int cap, int scratch,
+                                                          int* __restrict__ slots, int* __restrict__ pos,
+                                                          int* __restrict__ act, float* __restrict__ temp,
+                                                          int* __restrict__ topk, int* __restrict__ greedy,
+                                                          long long* __restrict__ seeds, long long* __restrict__ sstep,
+                                                          int* tin) {
+  extern __shared__ int gath[];
+  const int n = buf[4 * cap];
+  const int* f = buf + 4 * cap + 1;
+  const long long* s64 = reinterpret_cast<const long long*>(buf);
+  for (int i = threadIdx.x; i < b; i += blockDim.x) {
+    const bool live = i < n;
+    slots[i] = live ? f[i] : scratch;
+    pos[i] = live ? f[cap + i] : 0;
+    act[i] = live ? 1 : 0;
+    if (temp != nullptr) {
+      temp[i] = live ? __int_as_float(f[2 * cap + i]) : 1.0f;
+      topk[i] = live ? f[3 * cap + i] : 1;
+      greedy[i] = live ? f[4 * cap + i] : 1;
+      seeds[i] = live ? s64[i] : 0;
+      sstep[i] = live ? s64[cap + i] : 0;
+    }
+    if (tin != nullptr) gath[i] = tin[live ? f[5 * cap + i] : 0];
+  }
+  if (tin == nullptr) return;  // uniform across the workgroup
+  __syncthreads();
+  for (int i = threadIdx.x; i < b; i += blockDim.x) tin[i] = gath[i];
+}
+
+}  // namespace lsd
+
+// args: the host int64 record [cap, scratch, buf, slots, pos, act, temp, topk,
+// greedy, seeds, sstep, tin] (device pointers; 0 = the field is absent on this
+// stage) -- the native executor passes the same record it got from Python.
+extern "C" hipError_t lsd_apply_rows(const int64_t* args, int b, hipStream_t st) {
+  if (b <= 0) return hipSuccess;
+  const int cap = (int)args[0];
+  if (b > cap || b > 16384 || args[2] == 0 || args[3] == 0 || args[4] == 0 || args[5] == 0) return hipErrorInvalidValue;
+  if (args[6] != 0 && (args[7] == 0 || args[8] == 0 || args[9] == 0 || args[10] == 0)) return hipErrorInvalidValue;
+  const unsigned threads = b >= 1024 ? 1024u : (unsigned)((b + 63) / 64 * 64);
+  const size_t lds = args[11] != 0 ? (size_t)b * sizeof(int) : 0;
+  auto P = [&](int k) { return reinterpret_cast<void*>(args[k]); };
+  hipLaunchKernelGGL(lsd::apply_rows_kernel, dim3(1), dim3(threads), lds, st, static_cast<const int*>(P(2)), b, cap,
+                     (int)args[1], static_cast<int*>(P(3)), static_cast<int*>(P(4)), static_cast<int*>(P(5)),
+                     static_cast<float*>(P(6)), static_cast<int*>(P(7)), static_cast<int*>(P(8)),
+                     static_cast<long long*>(P(9)), static_cast<long long*>(P(10)), static_cast<int*>(P(11)));
+  return hipGetLastError();
+}

@@ -14,6 +14,8 @@
 //   [busy-timing event]
 //   [token readout: D2H copy of the previous item's sampled ids into a pinned
 //    host buffer + completion event the scheduler polls]
+//   [composition change: host-to-device copy of the packed row state from a
+//    pinned buffer + the apply_rows scatter / token gather (elementwise.hip)]
 //   hipGraphLaunch of the item's decode graph (its captured loopback ops
 //    pass the enqueue handshake first and advance the host mirrors after)
 //   [busy-timing event]
@@ -34,6 +36,7 @@ void lsd_rccl_recv_raw(int64_t h, void* ptr, size_t bytes, int peer, hipStream_t
 void lsd_loop_recv_raw(int64_t chan, void* ptr, size_t bytes, hipStream_t st);          // loop_fabric.cpp
 void lsd_loop_io_wait(int64_t io);
 void lsd_loop_io_done(int64_t io);
+extern "C" hipError_t lsd_apply_rows(const int64_t* args, int b, hipStream_t st);  // elementwise.hip
 
 namespace {
 
@@ -57,6 +60,10 @@ enum : int {
   X_T1,          // busy-timing event after the item
   X_RLOOP,       // token-return receive on a loopback channel (instead of X_RCOMM)
   X_IO,          // loopback I/O list captured in the graph (enqueue handshake + mirrors)
+  X_ROWS_ARGS,   // composition change: host int64 record of lsd_apply_rows (its [2] = device buffer)
+  X_ROWS_SRC,    //   pinned host source of the packed row state
+  X_ROWS_BYTES,  //   bytes
+  X_ROWS_B,      //   bucket rows
   X_FIELDS
 };
 
@@ -77,6 +84,13 @@ void lsd_register_exec(py::module& m) {
                                  (size_t)it[X_BYTES], hipMemcpyDeviceToHost, st),
                   "hipMemcpyAsync");
         hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(it[X_EV]), st), "hipEventRecord");
+      }
+      if (it[X_ROWS_ARGS]) {
+        const auto* args = reinterpret_cast<const int64_t*>(it[X_ROWS_ARGS]);
+        hip_check(hipMemcpyAsync(reinterpret_cast<void*>(args[2]), reinterpret_cast<const void*>(it[X_ROWS_SRC]),
+                                 (size_t)it[X_ROWS_BYTES], hipMemcpyHostToDevice, st),
+                  "hipMemcpyAsync");
+        hip_check(lsd_apply_rows(args, (int)it[X_ROWS_B], st), "apply_rows");
       }
       if (!it[X_GRAPH]) throw std::invalid_argument("exec_items: item without a graph");
       if (it[X_IO]) lsd_loop_io_wait(it[X_IO]);  // instant: the caller pre-waited the step's ops

@@ -217,7 +217,13 @@ class GroupState(racecheck.Shared):
         self.pf_pin: List[list] = []  # [pinned int32 staging, event of its last copy] ring
         self.pf_pin_next = 0
         self._metas: Dict[tuple, BatchMeta] = {}
-        self.rows_n = 0
+        # composition changes on a GPU (StageWorker._rows_pack): pinned packed
+        # row-state ring [pinned int32, event of its last copy, used], the
+        # device copy and the apply_rows argument record
+        self.rows_pin: List[list] = []
+        self.rows_pin_next = 0
+        self.rows_dev: Optional[torch.Tensor] = None
+        self.rows_args: Optional[torch.Tensor] = None
 
     def wire_buf(self, w: "StageWorker", b: int) -> Optional[torch.Tensor]:
         """Persistent wire-dtype staging rows of the decode receive (graph I/O)."""
@@ -383,6 +389,7 @@ class StageWorker(racecheck.Shared):
         self._tev_free: List[torch.cuda.Event] = []  # busy-timing events
         self._tev_used: List[torch.cuda.Event] = []
         self.native_steps = 0
+        self.native_changes = 0  # composition-change items issued by exec_items
         self.io_items = 0  # decode items whose (graph) body carried its own transfers
 
     # ------------------------------------------------------------------
@@ -566,7 +573,9 @@ class StageWorker(racecheck.Shared):
             return False
         descs = []
         for gp in items:
-            if gp.kind == "fwd_b" or gp.chunks or gp.rows is not None or gp.b <= 0 or gp.n_final:
+            if gp.kind == "fwd_b" or gp.chunks or gp.b <= 0 or gp.n_final:
+                return False
+            if gp.rows is not None and (not hasattr(self.stage.backend, "C") or gp.n > gp.b):
                 return False
             io = self._io(gp)
             if self.P > 1 and not io:
@@ -591,7 +600,7 @@ class StageWorker(racecheck.Shared):
         # handshake here, outside the gate; exec_items' own checks are then
         # instant (csrc/loop_fabric.cpp)
         pre: List[tuple] = []
-        rows, reads = [], []
+        rows, reads, packed = [], [], []
         recv_kind = []
         for gp, gs, g, ret, gio in descs:
             rk = None
@@ -628,6 +637,13 @@ class StageWorker(racecheck.Shared):
                     ev = self._new_event(False)
                     d[7], d[8], d[9], d[10] = gs.tin.data_ptr(), host.data_ptr(), 4 * ret, ev.cuda_event
                     reads.append((gp, host, ev))
+                if gp.rows is not None:
+                    # composition change: packed row state copied and applied
+                    # after the readout, ahead of the graph (csrc/stage_exec.cpp)
+                    slot, args = self._rows_pack(gs, gp.rows, gp.b)
+                    d[14], d[15], d[16], d[17] = args.data_ptr(), slot[0].data_ptr(), 4 * (10 * gs.cap + 1), gp.b
+                    packed.append((slot, lane))
+                    self.native_changes += 1
                 rows.append(d)
             try:
                 with (self.t.issuing() if self.t is not None else contextlib.nullcontext()):
@@ -638,6 +654,9 @@ class StageWorker(racecheck.Shared):
                 for lane in self.lanes:
                     lane.synchronize()
                 raise
+            for slot, lane in packed:
+                slot[1].record(lane)
+                slot[2] = True
         for gp, host, ev in reads:
             self.readout_native(plan, gp, host, ev, self._ev_free.append)
         self.native_steps += 1
@@ -822,8 +841,15 @@ class StageWorker(racecheck.Shared):
         act = [1] * n + [0] * pad
         if b == 0:
             return
-        gs.rows_n = n
         if dev.type == "cuda":
+            if hasattr(self.stage.backend, "C"):
+                slot, args = self._rows_pack(gs, rows, b)
+                words = 10 * gs.cap + 1
+                gs.rows_dev.copy_(slot[0][:words], non_blocking=True)
+                self.stage.backend.C.apply_rows(args, b)
+                slot[1].record()
+                slot[2] = True
+                return
             self._apply_rows_staged(gs, rows, b, pad, sl, pos, act)
             return
         gs.slots[:b].copy_(_h2d(sl, torch.int32, dev), non_blocking=True)
@@ -844,6 +870,52 @@ class StageWorker(racecheck.Shared):
             src = _h2d([r.src for r in rows] + [0] * pad, torch.int64, dev)
             gathered = gs.tin.index_select(0, src.to(dev, non_blocking=True))
             gs.tin[:b].copy_(gathered)
+
+    _ROWS_PIN = 4  # packed row-state buffers per group: reused 4 composition changes later
+
+    def _rows_pack(self, gs: GroupState, rows, b: int):
+        """Composition change on a GPU, host side: the new rows' state packed
+        into one pinned int32 buffer in the layout of elementwise.hip
+        apply_rows_kernel (fixed offsets by the group capacity, so the device
+        copy and the kernel depend on the bucket only), and the kernel's
+        argument record.  -> (pinned ring slot, CPU int64[12] record); the
+        caller enqueues the copy + kernel (eagerly, or in exec_items) and then
+        records the slot's event."""
+        cap = gs.cap
+        words = 10 * cap + 1
+        if len(gs.rows_pin) < self._ROWS_PIN:
+            gs.rows_pin.append([torch.empty(words, dtype=torch.int32, pin_memory=True), torch.cuda.Event(), False])
+        slot = gs.rows_pin[gs.rows_pin_next % len(gs.rows_pin)]
+        gs.rows_pin_next += 1
+        if slot[2]:
+            slot[1].synchronize()  # its previous copy has long landed
+        a = slot[0].numpy()
+        n = len(rows)
+        a[4 * cap] = n
+        if n:
+            f0 = 4 * cap + 1
+            a[f0: f0 + n] = [r.slot for r in rows]
+            a[f0 + cap: f0 + cap + n] = [r.pos for r in rows]
+            if self.last:
+                a[f0 + 2 * cap: f0 + 2 * cap + n] = np.asarray([r.temperature for r in rows], np.float32).view(np.int32)
+                a[f0 + 3 * cap: f0 + 3 * cap + n] = [r.top_k for r in rows]
+                a[f0 + 4 * cap: f0 + 4 * cap + n] = [1 if r.greedy else 0 for r in rows]
+                a64 = a[: 4 * cap].view(np.int64)
+                a64[:n] = [r.seed for r in rows]
+                a64[cap: cap + n] = [r.step for r in rows]
+            if self.first:
+                a[f0 + 5 * cap: f0 + 5 * cap + n] = [r.src for r in rows]
+        if gs.rows_dev is None:
+            gs.rows_dev = torch.empty(words, dtype=torch.int32, device=self.device)
+            gs.rows_args = torch.zeros(12, dtype=torch.int64)
+        r = gs.rows_args.numpy()
+        ptr = lambda t: t.data_ptr()  # noqa: E731
+        r[0], r[1], r[2] = cap, self.scratch_slot, ptr(gs.rows_dev)
+        r[3], r[4], r[5] = ptr(gs.slots), ptr(gs.pos), ptr(gs.active)
+        if self.last:
+            r[6], r[7], r[8], r[9], r[10] = ptr(gs.temp), ptr(gs.topk), ptr(gs.greedy), ptr(gs.seeds), ptr(gs.sstep)
+        r[11] = ptr(gs.tin) if self.first else 0
+        return slot, gs.rows_args
 
     def _apply_rows_staged(self, gs: GroupState, rows, b: int, pad: int, sl, pos, act) -> None:
         """_apply_rows on a GPU: every per-row field packed into ONE int32

@@ -294,7 +294,8 @@ def test_native_stage_executor_matches_python_item_loop(monkeypatch, timing):
     (csrc/stage_exec.cpp: one C++ call per step -- graph launches, token
     readout copies, busy-timing events) and give the Python item loop's tokens
     bit for bit, with and without per-item timing events; EOS stops and
-    sequences leaving mid-session fall back to the Python loop for that step."""
+    sequences leaving mid-session (composition changes) are issued natively
+    too: packed row state + apply_rows ahead of the graph."""
     prompts = [[1, 2, 3, 4], [5, 6], list(range(10, 50)), [7] * 9, [3, 3]]
     sps = [SamplingParams(temperature=0.8, top_k=20, seed=5, max_new_tokens=n) for n in (12, 5, 16, 9, 1)]
     monkeypatch.setenv("LSD_NATIVE_EXEC", "0")
@@ -307,5 +308,6 @@ def test_native_stage_executor_matches_python_item_loop(monkeypatch, timing):
     got = nat.generate_ids(prompts, sps, record_timing=timing)  # graphs cached: native steps
     assert got == want
     assert sum(w.native_steps for w in nat.workers) > 0
+    assert sum(w.native_changes for w in nat.workers) > 0
     if timing:
         assert nat.last_session is not None and 0.0 < nat.last_session.stages[0]["busy_fraction"] <= 1.0

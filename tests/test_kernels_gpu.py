@@ -964,3 +964,61 @@ def test_attention_oproj_fused(C, CNT, hd, nh, n_kv, N, B, nc):
     C.attn_oproj(q, kc, vc, seq_slots, pos, nh, w, None, x3, nc, CNT)  # no bias
     close(x3 - x0, y_ref - bias.float().cpu(), 2e-2)
     assert int(CNT.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("cap,b,n,first,last", [(256, 256, 256, True, True), (256, 128, 77, True, True),
+                                                (300, 64, 0, True, False), (2048, 2048, 1500, False, True),
+                                                (8, 8, 3, False, False)])
+def test_apply_rows(C, cap, b, n, first, last):
+    """Composition change of a decode group (elementwise.hip apply_rows_kernel):
+    the packed row state scattered into the row vectors, pad rows [n, b) idle
+    on the scratch slot, stage 0's in-place token gather (sources anywhere in
+    the previous return vector, including rows this launch overwrites) -- vs
+    the same fields written from Python lists."""
+    import numpy as np
+
+    g = torch.Generator().manual_seed(cap + b + n)
+    scratch = 12345
+    ri = lambda lo, hi, k: torch.randint(lo, hi, (k,), generator=g)  # noqa: E731
+    slot, pos, topk, greedy, src = ri(0, 10000, n), ri(0, 4096, n), ri(1, 64, n), ri(0, 2, n), ri(0, cap, n)
+    temp = torch.rand(n, generator=g) + 0.1
+    seed, step = ri(0, 1 << 62, n), ri(0, 1 << 40, n)
+    a = np.zeros(10 * cap + 1, np.int32)
+    a[: 4 * cap].view(np.int64)[:n] = seed.numpy()
+    a[: 4 * cap].view(np.int64)[cap: cap + n] = step.numpy()
+    a[4 * cap] = n
+    f0 = 4 * cap + 1
+    for k, v in enumerate((slot, pos, None, topk, greedy, src)):
+        if v is not None:
+            a[f0 + k * cap: f0 + k * cap + n] = v.numpy()
+    a[f0 + 2 * cap: f0 + 2 * cap + n] = temp.numpy().astype(np.float32).view(np.int32)
+    i32 = dict(dtype=torch.int32, device=DEV)
+    buf = torch.from_numpy(a).to(DEV)
+    t = dict(slots=torch.full((cap,), -1, **i32), pos=torch.full((cap,), -1, **i32), act=torch.full((cap,), -1, **i32))
+    if last:
+        t.update(temp=torch.zeros(cap, device=DEV), topk=torch.zeros(cap, **i32), greedy=torch.zeros(cap, **i32),
+                 seeds=torch.full((cap,), -1, dtype=torch.int64, device=DEV),
+                 sstep=torch.full((cap,), -1, dtype=torch.int64, device=DEV))
+    tin0 = ri(0, 50000, cap).to(torch.int32)
+    tin = tin0.to(DEV)
+    ptr = lambda k: t[k].data_ptr() if k in t else 0  # noqa: E731
+    args = torch.tensor([cap, scratch, buf.data_ptr(), ptr("slots"), ptr("pos"), ptr("act"), ptr("temp"), ptr("topk"),
+                         ptr("greedy"), ptr("seeds"), ptr("sstep"), tin.data_ptr() if first else 0], dtype=torch.int64)
+    C.apply_rows(args, b)
+    torch.cuda.synchronize()
+    pad = b - n
+    cat = lambda v, fill: torch.cat([v.to(torch.int64), torch.full((pad,), fill, dtype=torch.int64)])  # noqa: E731
+    assert torch.equal(t["slots"][:b].cpu().long(), cat(slot, scratch))
+    assert torch.equal(t["pos"][:b].cpu().long(), cat(pos, 0))
+    assert torch.equal(t["act"][:b].cpu().long(), cat(torch.ones(n, dtype=torch.int64), 0))
+    assert (t["slots"][b:] == -1).all()  # rows past the bucket untouched
+    if last:
+        assert torch.equal(t["temp"][:b].cpu(), torch.cat([temp.float(), torch.ones(pad)]))
+        assert torch.equal(t["topk"][:b].cpu().long(), cat(topk, 1))
+        assert torch.equal(t["greedy"][:b].cpu().long(), cat(greedy, 1))
+        assert torch.equal(t["seeds"][:b].cpu(), cat(seed, 0))
+        assert torch.equal(t["sstep"][:b].cpu(), cat(step, 0))
+    want = tin0.clone()
+    if first:
+        want[:b] = tin0[cat(src, 0)]
+    assert torch.equal(tin.cpu(), want)
