@@ -562,6 +562,10 @@ class StageWorker(racecheck.Shared):
         return ring[k, :n]
 
     _PIN_SLOTS = 64
+    # composition-change items (joins activating, leaves) on the native
+    # executor; LSD_NATIVE_CHANGES=0 sends them to the Python item loop (A/B,
+    # tools/serve_load.py)
+    NATIVE_CHANGES = os.environ.get("LSD_NATIVE_CHANGES", "1") == "1"
 
     def _native_step(self, plan: StepPlan, items: List[GroupPlan]) -> bool:
         """Enqueue this step with one C++ call (csrc/stage_exec.cpp exec_items)
@@ -575,7 +579,8 @@ class StageWorker(racecheck.Shared):
         for gp in items:
             if gp.kind == "fwd_b" or gp.chunks or gp.b <= 0 or gp.n_final:
                 return False
-            if gp.rows is not None and (not hasattr(self.stage.backend, "C") or gp.n > gp.b):
+            if gp.rows is not None and (not self.NATIVE_CHANGES or not hasattr(self.stage.backend, "C")
+                                        or gp.n > gp.b):
                 return False
             io = self._io(gp)
             if self.P > 1 and not io:
