@@ -168,7 +168,7 @@ def main() -> int:
     sync()
     if getattr(eng, "_phases", None):
         eng._phases.clear()
-        eng._hostprof[:] = [0.0, 0.0, 0.0, 0, 0, 0.0, 0.0, 0]
+        eng._hostprof[:] = [0.0] * len(eng._hostprof)
     t0 = time.perf_counter()
     step_ms, prefill_ms, max_step, decode_sum = [], [], [], []
     for _ in range(args.steps):

@@ -120,7 +120,10 @@ class Engine(racecheck.Shared):
         self._wake = threading.Event()  # a request was submitted (serving loop)
         # LSD_HOST_PROFILE=1: host seconds in (plan, issue, readout wait), steps,
         # items, issuing-thread CPU, plan-send seconds, plan bytes sent
-        self._hostprof = [0.0, 0.0, 0.0, 0, 0, 0.0, 0.0, 0] if os.environ.get("LSD_HOST_PROFILE") == "1" else None
+        # [plan s, issue s, readout wait s, decode steps, items, issuing CPU s, plan send s, plan bytes,
+        #  then steps with prefill chunks: issue s, readout wait s, steps]
+        self._hostprof = ([0.0, 0.0, 0.0, 0, 0, 0.0, 0.0, 0, 0.0, 0.0, 0]
+                          if os.environ.get("LSD_HOST_PROFILE") == "1" else None)
         # LSD_HOST_PROFILE: host-clock seconds per session phase, summed over sessions
         self._phases: Optional[Dict[str, float]] = {} if self._hostprof is not None else None
         self.kv_slots = 0
@@ -484,8 +487,13 @@ class Engine(racecheck.Shared):
                 t2 = time.monotonic()
                 c2 = time.thread_time() if hp is not None else 0.0
                 sch.poll(block_until_step=cur[0].step - lag)
-                if hp is not None and not any(gp.chunks for gp in cur[0].groups):
-                    t3 = time.monotonic()  # decode steps only (prefill issue is eager)
+                if hp is not None and any(gp.chunks for gp in cur[0].groups):
+                    t3 = time.monotonic()  # steps with prefill chunks (eager issue)
+                    hp[8] += t2 - t1
+                    hp[9] += t3 - t2
+                    hp[10] += 1
+                elif hp is not None:
+                    t3 = time.monotonic()  # decode-only steps
                     hp[0] += t1 - t0
                     hp[1] += t2 - t1
                     hp[2] += t3 - t2

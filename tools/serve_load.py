@@ -36,7 +36,8 @@ def main():
     gl, gh = map(int, a.gen.split(","))
     C = a.concurrency
     cfg = EngineConfig(model_id=a.model, num_stages=1, max_batch=C, max_seq_len=ph + gh,
-                       num_microbatches=a.microbatches, device=a.device, seed=a.seed)
+                       num_microbatches=a.microbatches, device=a.device, seed=a.seed,
+                       metrics_every=1)  # per-stage busy fraction of the serving session
     eng = Engine(cfg)
     rnd = random.Random(a.seed)
     V = eng.mcfg.vocab_size
@@ -51,6 +52,8 @@ def main():
     warm = [make() for _ in range(C)]
     eng.generate_ids([w[0] for w in warm], [w[1] for w in warm])
     freeze_gc()
+    if getattr(eng, "_hostprof", None) is not None:
+        eng._hostprof[:] = [0.0] * len(eng._hostprof)
     eng.start_loop()
     st0 = eng.scheduler.stats["steps"]
     n0 = sum(w.native_steps for w in eng.workers), sum(w.native_changes for w in eng.workers)
@@ -82,7 +85,16 @@ def main():
         "ttft_ms_p90": round(q(ttft, 0.9), 2), "steps": eng.scheduler.stats["steps"] - st0,
         "native_steps": sum(w.native_steps for w in eng.workers) - n0[0],
         "native_changes": sum(w.native_changes for w in eng.workers) - n0[1],
-        "native_changes_env": os.environ.get("LSD_NATIVE_CHANGES", "1")}), flush=True)
+        "native_changes_env": os.environ.get("LSD_NATIVE_CHANGES", "1"),
+        "stage0_busy": (eng.last_session.stages[0]["busy_fraction"] if eng.last_session is not None
+                        and eng.last_session.stages else None)}), flush=True)
+    hp = getattr(eng, "_hostprof", None)
+    if hp is not None and hp[3]:
+        print(f"host per decode-only step: plan {hp[0] / hp[3] * 1e6:.1f} us, issue {hp[1] / hp[3] * 1e6:.1f} us, "
+              f"readout wait {hp[2] / hp[3] * 1e6:.1f} us over {hp[3]} steps", flush=True)
+    if hp is not None and hp[10]:
+        print(f"host per step with prefill chunks: issue {hp[8] / hp[10] * 1e6:.1f} us, readout wait "
+              f"{hp[9] / hp[10] * 1e6:.1f} us over {hp[10]} steps", flush=True)
     eng.shutdown()
 
 
