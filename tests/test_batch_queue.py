@@ -73,3 +73,24 @@ def test_stress_under_sanitizers(tmp_path, san):
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert "ThreadSanitizer" not in r.stderr and "ERROR" not in r.stderr
     assert r.stdout.startswith("ok ")
+
+
+def test_push_many_matches_push_on_both_queues(R):
+    """push_many (one lock, one wake-up; the scheduler's bulk admission) queues
+    exactly what the same pushes one by one would, on the native queue and its
+    Python twin; refused as a whole once closed; length mismatch rejected."""
+    rnd = random.Random(3)
+    items = [(i, rnd.choice([0, 1, 2, 5, 8, 30, 100, 400])) for i in range(70)]
+    ids, lens = [i for i, _ in items], [n for _, n in items]
+    for make in (lambda: R.BatchQueue(32, 4.0), lambda: PyBatchQueue(32, 4.0)):
+        one, bulk = make(), make()
+        for i, n in items:
+            one.push(i, n)
+        assert bulk.push_many(ids[:40], lens[:40]) and bulk.push_many(ids[40:], lens[40:])
+        assert bulk.depth == one.depth == 70 and bulk.pushed == one.pushed == 70
+        for _ in range(3):
+            assert bulk.next_groups(0.0) == one.next_groups(0.0)
+        with pytest.raises(ValueError):
+            bulk.push_many([1, 2], [3])
+        bulk.close()
+        assert not bulk.push_many([5], [5]) and bulk.drain() == []

@@ -162,3 +162,25 @@ def test_core_stress_under_asan_ubsan(tmp_path):
     r = subprocess.run([str(exe), "40"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert r.stdout.startswith("ok 40")
+
+
+def test_add_many_matches_add():
+    """SchedCore.add_many (bulk admission) == add() one by one, native and
+    Python twin: same plans; an empty prompt anywhere rejects the whole batch."""
+    rt = _rt()
+    seqs = [(i, 1 + (7 * i) % 23, 1 + (5 * i) % 9, i % 2 == 0) for i in range(20)]
+    plans = []
+    for core in ("native", "py"):
+        for bulk in (False, True):
+            pool = [rt.SlotAllocator(16)] if core == "native" else [PySlots(16)]
+            c = (rt.SchedCore if core == "native" else PySchedCore)(1, 2, 4, 0, 0, 512, pool)
+            if bulk:
+                c.add_many(*map(list, zip(*seqs)))
+                with pytest.raises(ValueError):
+                    c.add_many([99, 100], [3, 0], [1, 1], [False, False])
+            else:
+                for s in seqs:
+                    c.add(*s)
+            p, adm = c.plan(0)
+            plans.append(([[(tuple(go[:6]), [tuple(x) for x in go[6]]) for go in rep] for rep in p], list(adm)))
+    assert all(p == plans[0] for p in plans[1:])

@@ -217,3 +217,37 @@ def test_watchdog_aborts_data_plane_on_async_error_and_timeout():
         time.sleep(0.02)
     wd2.close()
     assert not eng2.healthy and eng2.last_error.startswith("WatchdogTimeout") and tr2.aborts == 1
+
+
+def test_bulk_submit_matches_one_by_one_and_converts_ids():
+    """generate_ids admits a batch through Scheduler.submit_many (one pass,
+    native push_many / add_many): same tokens as submitting one by one, numpy
+    token ids converted, zero-token requests finished at once."""
+    import numpy as np
+
+    from llm_sharding_demo_amd.runtime.scheduler import Request
+
+    prompts = [[5, 6, 7], np.array([9, 8], dtype=np.int64), [1] * 7, [4, 4]]
+    sps = [SamplingParams(temperature=0.7, top_k=10, seed=s, max_new_tokens=n) for s, n in
+           ((1, 5), (2, 3), (3, 0), (4, 6))]
+    e = _engine(max_batch=8)
+    bulk = e.generate_ids(prompts, sps)
+    assert bulk[2] == [] and [len(t) for t in bulk] == [5, 3, 0, 6]
+    e2 = _engine(max_batch=8)
+    reqs = [e2.submit(list(map(int, p)), sp) for p, sp in zip(prompts, sps)]
+    e2.start_loop()
+    try:
+        assert [r.wait(60) for r in reqs] == bulk
+    finally:
+        e2.stop_loop()
+    reqs = e.scheduler.submit_many([np.array([3, 2], dtype=np.int32)], [sps[0]])
+    assert reqs[0].prompt_ids == [3, 2] and all(type(t) is int for t in reqs[0].prompt_ids)
+    e.scheduler.fail_all(RuntimeError("drop"))
+    with pytest.raises(RuntimeError, match="drop"):
+        reqs[0].wait(1)
+    # the completion event is made lazily: a waiter blocked before finish() wakes up
+    r = Request([1], sps[0])
+    threading.Timer(0.05, lambda: r.finish([7])).start()
+    assert r.wait(5) == [7] and r.done
+    with pytest.raises(RequestTimeout):
+        Request([1], sps[0]).wait(0.01)
