@@ -529,11 +529,12 @@ class GlooPlanChannel:
     posts blocking receives from its single source in FIFO order.
     `plans=False` selects the plain pickled-object channel."""
 
-    def __init__(self, group, tag: int = 1, plans: bool = True):
+    def __init__(self, group, tag: int = 1, plans: bool = True, stages: Optional[int] = None):
         import torch.distributed as dist
 
         self.dist, self.pg, self.tag = dist, group, tag
         self.plans = plans
+        self.P = stages  # pipeline stages per replica (None: send token ids everywhere)
         # posted sends, oldest first; completed ones are dropped from the
         # front (a scan of the whole list per send cost ~2 ms per step at
         # 7 followers x 64 steps of look-ahead: profiles/r4_plan_wire.log)
@@ -554,7 +555,8 @@ class GlooPlanChannel:
 
             enc = self._enc.get(dst)
             if enc is None:
-                enc = self._enc[dst] = PlanEncoder()
+                # token ids only to a replica's first stage
+                enc = self._enc[dst] = PlanEncoder(ids=self.P is None or dst % self.P == 0)
             rec, payload = enc.encode(obj)
             hdr = torch.from_numpy(rec)
             works = [self._isend(hdr, dst, self.tag), hdr]
@@ -664,7 +666,8 @@ class ShmPlanChannel:
             raise TransportError(f"shared-memory plan ring unavailable: {err or errs}")
         from ..runtime.plan import PlanDecoder, PlanEncoder
 
-        self._enc = {rep: PlanEncoder() for rep in self.rings}
+        # replica 0's stage 0 is rank 0 itself: its followers never read token ids
+        self._enc = {rep: PlanEncoder(ids=rep > 0) for rep in self.rings}
         self._dec = PlanDecoder()
         self.fallback = GlooPlanChannel(transport.plan_pg, tag=1, plans=False)
         self.bytes_sent = 0
@@ -744,7 +747,7 @@ def make_plan_channel(transport: "_DistTransport", timeout_s: float):
             # all of them fall back together
             logging.getLogger("llm_sharding_demo_amd.comm").warning(
                 "shared-memory plan ring unavailable (%s): plans over gloo", e)
-    return GlooPlanChannel(transport.plan_pg, tag=1, plans=wire != "pickle")
+    return GlooPlanChannel(transport.plan_pg, tag=1, plans=wire != "pickle", stages=transport.P)
 
 
 # ---------------------------------------------------------------------------

@@ -55,3 +55,40 @@ def test_random_plan_streams():
         kinds[int(rec[0])] += 1
         assert out == plan
     assert kinds[MAGIC_REPEAT] > kinds[MAGIC_STEADY] > 0 and kinds[MAGIC_PICKLE] > 0
+
+
+def test_columnar_groups_and_token_ids_only_where_read():
+    """Non-steady plans travel with each GroupPlan as columns (runtime/plan.py
+    _pack_group): exact round trip of every Chunk / Row field (large seeds,
+    fp64 temperatures, greedy flags, rows=[] vs None); an encoder for stages
+    that never read prefill token ids (ids=False) sends the chunk lengths only,
+    and its payload is several times smaller."""
+    rnd = random.Random(5)
+
+    def chunk(i):
+        n = rnd.randint(1, 40)
+        return Chunk(i, rnd.randrange(4096), rnd.randrange(512), [rnd.randrange(50257) for _ in range(n)],
+                     rnd.random() < 0.5, rnd.random() + 0.05, rnd.randint(1, 64), rnd.random() < 0.3,
+                     rnd.randrange(1 << 62))
+
+    def row(i):
+        return Row(i, rnd.randrange(4096), rnd.randrange(1024), rnd.random() + 0.05, rnd.randint(1, 64),
+                   rnd.random() < 0.3, rnd.randrange(1 << 62), rnd.randrange(1 << 40), rnd.randrange(512))
+
+    plan = StepPlan(step=3, replica=1, timing=True, groups=[
+        GroupPlan(0, ret=5, n=4, b=8, ctxb=256, chunks=[chunk(i) for i in range(300)], rows=[row(i) for i in range(7)]),
+        GroupPlan(1, ret=0, n=0, b=0, ctxb=0, rows=[]),
+        GroupPlan(2, ret=2, n=2, b=2, ctxb=256, chunks=[chunk(1000)]),
+        GroupPlan(3, kind="fwd_b", fwd_rows=9)])
+    rec, out = _rt(PlanEncoder(), PlanDecoder(), plan)
+    assert rec[0] == MAGIC_PICKLE and out == plan
+    assert out.groups[1].rows == [] and out.groups[2].rows is None
+    full = rec[1]
+    rec, out = _rt(PlanEncoder(ids=False), PlanDecoder(), plan)
+    assert rec[1] * 2 < full
+    for a, b in zip(out.groups, plan.groups):
+        assert [c.qlen for c in a.chunks] == [c.qlen for c in b.chunks]
+        assert [(c.seq, c.slot, c.start, c.final, c.temperature, c.top_k, c.greedy, c.seed) for c in a.chunks] == \
+            [(c.seq, c.slot, c.start, c.final, c.temperature, c.top_k, c.greedy, c.seed) for c in b.chunks]
+        assert a.rows == b.rows and (a.g, a.ret, a.n, a.b, a.ctxb, a.kind, a.fwd_rows) == \
+            (b.g, b.ret, b.n, b.b, b.ctxb, b.kind, b.fwd_rows)
