@@ -37,6 +37,8 @@ class Routing:
     gemv_nt: int = 0  # non-temporal weight loads in the GEMV (A/B)
     # -- decode attention --------------------------------------------------
     target_blocks: int = 512  # >> 256 CUs: VALU decode attention splits the context up to this
+    split_keys: int = 256      # ... with at least this many keys per split (64 / 128 lose at 1-16
+    #                            sequences: the combine launch costs more, r6_split_keys.log)
     # grouped-query decode attention on MFMA (attn_decode_mfma_kernel) at >=
     # attn_mfma_min waves; fewer than attn_mfma_split_below items split the
     # context towards attn_mfma_waves waves, >= 512 keys per split (Llama-3
@@ -252,7 +254,7 @@ class Routing:
             if items * ms >= self.attn_mfma_min:
                 return ms
         if items < self.target_blocks:
-            return min(math.ceil(self.target_blocks / items), max(1, math.ceil(max_ctx / 256)))
+            return min(math.ceil(self.target_blocks / items), max(1, math.ceil(max_ctx / self.split_keys)))
         return 1
 
 
