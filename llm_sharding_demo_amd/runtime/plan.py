@@ -25,6 +25,8 @@ mode), so all stages agree on shapes without any device->host sync.
 """
 from __future__ import annotations
 
+import io
+import pickle
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -185,18 +187,22 @@ def _unpack_group(g, ret, n, b, ctxb, kind, fwd_rows, ch, rows) -> GroupPlan:
     return gp
 
 
+class _PlanPickler(pickle.Pickler):
+    """Pickles every GroupPlan through _pack_group (ids: with token ids)."""
+
+    def __init__(self, file, ids: bool):
+        super().__init__(file, protocol=pickle.HIGHEST_PROTOCOL)
+        self.ids = ids
+
+    def reducer_override(self, obj):
+        if type(obj) is GroupPlan:
+            return _unpack_group, _pack_group(obj, self.ids)
+        return NotImplemented
+
+
 def _plan_dumps(plan: StepPlan, ids: bool) -> bytes:
-    import io
-    import pickle
-
-    class _P(pickle.Pickler):
-        def reducer_override(self, obj):
-            if type(obj) is GroupPlan:
-                return _unpack_group, _pack_group(obj, ids)
-            return NotImplemented
-
     buf = io.BytesIO()
-    _P(buf, protocol=pickle.HIGHEST_PROTOCOL).dump(plan)
+    _PlanPickler(buf, ids).dump(plan)
     return buf.getvalue()
 
 
@@ -243,8 +249,6 @@ class PlanDecoder:
         """rec: int32 sequence of PLAN_WORDS; fetch_payload(nbytes) -> bytes."""
         magic = int(rec[0])
         if magic == MAGIC_PICKLE:
-            import pickle
-
             self._prev = None
             # our own plan records, produced by this job's rank 0
             return pickle.loads(fetch_payload(int(rec[1])))
