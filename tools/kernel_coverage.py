@@ -1,4 +1,5 @@
-"""GPU occupancy from a rocprofv3 kernel trace: the union of all kernel
+"""GPU occupancy from a rocprofv3 kernel trace (the whole-session variant of
+gap_union.py, which attributes the gaps of a short window): the union of all kernel
 intervals (any stream) against the wall span, over the whole trace and over
 the longest stretch of decode-step kernels.  Gaps = the device running
 nothing (host issue, synchronisation, transfers outside kernels).
