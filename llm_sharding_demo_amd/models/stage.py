@@ -99,6 +99,13 @@ class StageModel:
         """Attention + output projection + residual add: one fused launch when
         the backend has it for this shape (small decode batches), else two."""
         be = self.backend
+        dec = getattr(meta, "dec", None)
+        if dec is not None:  # mixed step (runtime/batch.py MixedMeta): each part its own kernel
+            b = meta.b
+            o = torch.cat([be.attention(q[:b], self.kv.k(li), self.kv.v(li), dec),
+                           be.attention(q[b:], self.kv.k(li), self.kv.v(li), meta.pf)])
+            be.linear_residual(o, wo, bo, r)
+            return
         fused = getattr(be, "attention_oproj", None)
         if fused is not None and fused(q, self.kv.k(li), self.kv.v(li), meta, wo, bo, r):
             return
@@ -144,7 +151,9 @@ class StageModel:
         group's parity under alternating splits; 0 otherwise)."""
         x = self.embed(inp, meta) if self.first else inp
         r = Residual(x)
-        self.backend.decode = meta.is_decode  # decode-only routing rules (ops/hip.py)
+        # decode-only routing rules (ops/hip.py); a mixed step's rows follow them up to 512
+        self.backend.decode = getattr(meta, "routing_decode", meta.is_decode) and meta.num_tokens <= 512 \
+            if getattr(meta, "dec", None) is not None else meta.is_decode
         gpt2 = self.cfg.arch == "gpt2"
         attn_fn = self._gpt2_attn if gpt2 else self._llama_attn
         mlp_fn = self._gpt2_mlp if gpt2 else self._llama_mlp

@@ -42,7 +42,7 @@ import numpy as np
 import torch
 
 from ..models.stage import StageModel
-from ..runtime.batch import BatchMeta, SamplingState
+from ..runtime.batch import BatchMeta, MixedMeta, SamplingState
 from ..runtime.plan import GroupPlan, StepPlan
 from ..utils.tracing import trace_range
 from ..utils import racecheck
@@ -390,6 +390,7 @@ class StageWorker(racecheck.Shared):
         self._tev_used: List[torch.cuda.Event] = []
         self.native_steps = 0
         self.native_changes = 0  # composition-change items issued by exec_items
+        self.mixed_items = 0     # decode + prefill items run as one forward (_mixed)
         self.io_items = 0  # decode items whose (graph) body carried its own transfers
 
     # ------------------------------------------------------------------
@@ -799,6 +800,9 @@ class StageWorker(racecheck.Shared):
         # --- composition change: rewrite the decode rows' state
         if gp.rows is not None:
             self._apply_rows(gp, gs)
+        if gp.chunks and gp.b > 0 and self._mixed_ok(gp):
+            self._mixed(gp, gs)
+            return
         sends: List[torch.Tensor] = []
         finals = None
         # --- prefill chunks of joining sequences (eager)
@@ -832,6 +836,58 @@ class StageWorker(racecheck.Shared):
         else:
             for x in sends:
                 self.send_pending.setdefault(gp.g, []).append(self._send(x, self.r + 1, "fwd", lane))
+
+    # Mixed steps (one stage): a group whose step both decodes rows and
+    # prefills joining prompts runs ONE eager forward over [decode rows |
+    # chunk tokens] (runtime/batch.py MixedMeta) instead of the decode graph
+    # plus a second, prefill-only forward -- every weight is read once per
+    # step, and the GEMMs see b + T rows.  Continuous serving joins sequences
+    # at most steps (tools/serve_load.py); the bench's session shape (every
+    # sequence joins at step 0) never mixes.  Opt-in (LSD_MIXED_STEPS=1): the
+    # eager mixed forward gives up the decode rows' graph replay, and under
+    # the closed-loop serving load it measured slower on GPT-2 XL (34.2-35.5k
+    # vs 38.3-38.4k tok/s) and GPT-2 small, +1.4 % on Llama-3 8B
+    # (profiles/r6_mixed_steps.log).
+    MIXED_STEPS = os.environ.get("LSD_MIXED_STEPS", "0") == "1"
+
+    def _mixed_ok(self, gp: GroupPlan) -> bool:
+        return (getattr(self, "mixed_steps", self.MIXED_STEPS) and self.P == 1 and gp.kind == "step"
+                and gp.n <= gp.b)
+
+    def _mixed(self, gp: GroupPlan, gs: GroupState) -> None:
+        st, be, dev = self.stage, self.stage.backend, self.device
+        ch = gp.chunks
+        b = gp.b
+        pf, ids, _ = self._chunk_meta(gs, ch, tuple(c.qlen for c in ch))
+        dec = gs.meta(b, gp.ctxb)
+        mm = MixedMeta(token_slots=torch.cat([dec.token_slots, pf.token_slots]),
+                       token_pos=torch.cat([dec.token_pos, pf.token_pos]), b=b, dec=dec, pf=pf,
+                       num_tokens=b + pf.num_tokens)
+        inp = torch.cat([gs.tin[:b], ids])  # a copy: the samplers below overwrite tin (= tokret)
+        finals = [i for i, c in enumerate(ch) if c.final]
+        J = len(finals)
+        rows = torch.arange(b, dtype=torch.int32, device=dev)
+        if J:
+            fi = torch.tensor(finals, dtype=torch.long, device=dev)
+            rows = torch.cat([rows, pf.last_idx.index_select(0, fi) + b])
+        logits = st.forward(mm, inp, head=True, head_rows=rows, variant=gp.g & 1)
+        gs.ensure_tokret(self, b + J)
+        V = st.cfg.vocab_size
+        seg = getattr(logits, "_lsd_segmax", None)
+        ld = logits[:b]
+        if seg is not None:
+            ld._lsd_segmax = seg[:b]
+        # decode rows: draw, advance their sampler counters and positions (as the graph does)
+        be.sample_into(ld, gs.samp(b), V, gs.tokret[:b], dec)
+        if J:
+            lf = logits[b:]
+            if seg is not None:
+                lf._lsd_segmax = seg[b:]
+            fc = [ch[i] for i in finals]
+            samp = SamplingState([c.temperature for c in fc], [c.top_k for c in fc],
+                                 [c.greedy for c in fc], [c.seed for c in fc], dev)
+            gs.tokret[b: b + J].copy_(be.sample(lf, samp, V))
+        self.mixed_items += 1
 
     def _apply_rows(self, gp: GroupPlan, gs: GroupState) -> None:
         """New composition: rows [0, n) from the plan, pad rows [n, b) idle on

@@ -86,6 +86,27 @@ class BatchMeta:
             self.token_pos.add_(self.active)
 
 
+@dataclass
+class MixedMeta:
+    """One forward over a group's decode rows AND the prefill chunks joining
+    it in the same step (parallel/pipeline.py _mixed): rows [0, b) are the
+    decode rows (`dec`, the group's captured-bucket meta), rows [b, b + T) the
+    chunk tokens (`pf`).  Every row-wise op (norms, GEMMs, the QKV epilogue's
+    KV append at `token_slots` / `token_pos`) runs once over all rows, so the
+    weights are read once per step instead of once for the decode graph and
+    again for the prefill forward; the attention runs per part
+    (models/stage.py _attn_out)."""
+    token_slots: torch.Tensor  # int32 [b + T]
+    token_pos: torch.Tensor    # int32 [b + T]
+    b: int
+    dec: BatchMeta
+    pf: BatchMeta
+    num_tokens: int
+    is_decode: bool = False
+    routing_decode: bool = True  # decode-shaped routing rules while b + T <= 512 rows
+
+
+
 class SamplingState:
     """Per-row sampling parameters living on the device of the last stage.
 

@@ -251,3 +251,40 @@ def test_bulk_submit_matches_one_by_one_and_converts_ids():
     assert r.wait(5) == [7] and r.done
     with pytest.raises(RequestTimeout):
         Request([1], sps[0]).wait(0.01)
+
+
+@pytest.mark.parametrize("greedy", [True, False])
+def test_mixed_steps_match_separate_forwards(greedy):
+    """One stage: a group that decodes rows AND prefills joining prompts in the
+    same step runs one forward over both (pipeline.py _mixed, MixedMeta) --
+    same tokens as the decode graph + separate prefill forward, with seeded
+    sampling too; requests join a running batch at different steps."""
+    import random
+
+    rnd = random.Random(3)
+    prompts = [[rnd.randrange(1, 200) for _ in range(rnd.randint(2, 9))] for _ in range(12)]
+    sps = [SamplingParams(greedy=greedy, temperature=0.8, top_k=20, seed=100 + i,
+                          max_new_tokens=rnd.randint(2, 12)) for i in range(12)]
+
+    def run(mixed: bool):
+        e = _engine(P=1, max_batch=16, num_microbatches=2)
+        for w in e.workers:
+            w.mixed_steps = mixed
+        e.start_loop()
+        try:
+            reqs = []
+            for i, (p, sp) in enumerate(zip(prompts, sps)):
+                reqs.append(e.submit(p, sp))
+                if i % 3 == 2:  # let the running batch advance before more join
+                    st = e.scheduler.stats["steps"]
+                    while e.scheduler.stats["steps"] < st + 2 and not all(r.done for r in reqs):
+                        time.sleep(0.001)
+            out = [r.wait(60) for r in reqs]
+        finally:
+            e.stop_loop()
+        return out, sum(w.mixed_items for w in e.workers)
+
+    sep, n_sep = run(False)
+    mix, n_mix = run(True)
+    assert n_sep == 0 and n_mix > 0
+    assert mix == sep
