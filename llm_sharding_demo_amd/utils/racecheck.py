@@ -27,6 +27,7 @@ return the plain `threading` primitives and `Shared` is `object`: zero cost.
 """
 from __future__ import annotations
 
+import collections
 import os
 import threading
 import traceback
@@ -41,6 +42,13 @@ _state_lock = threading.Lock()
 _state: Dict[Tuple[int, str], list] = {}
 _final: set = set()  # ids with a finalizer registered
 _reports: List[dict] = []
+# ids of dead objects whose write history is still to be dropped: a finalizer
+# may run inside ANY allocation -- also one made while this thread holds
+# _state_lock (the weakref.finalize call in note() allocates, a collection
+# it triggers finalizes some other object) -- so finalizers only queue the id
+# (deque.append: atomic, takes no lock) and the next locked section drops it,
+# before it can look up a key of an object that reused the id
+_dead: "collections.deque[int]" = collections.deque()
 
 
 def _held() -> list:
@@ -123,6 +131,7 @@ def note(obj, field: str) -> None:
     held = frozenset(id(x) for x in _held())
     key = (id(obj), field)
     with _state_lock:
+        _drop_dead()
         st = _state.get(key)
         if st is None:
             _state[key] = [me, None, False]
@@ -147,7 +156,13 @@ def note(obj, field: str) -> None:
 
 
 def _forget(oid: int) -> None:
-    with _state_lock:
+    _dead.append(oid)
+
+
+def _drop_dead() -> None:
+    """Under _state_lock: drop the write history of the objects that died."""
+    while _dead:
+        oid = _dead.popleft()
         _final.discard(oid)
         for k in [k for k in _state if k[0] == oid]:
             del _state[k]
@@ -159,6 +174,7 @@ def handoff(obj) -> None:
         return
     oid = id(obj)
     with _state_lock:
+        _drop_dead()
         for k in [k for k in _state if k[0] == oid]:
             del _state[k]
 
@@ -170,6 +186,7 @@ def reports() -> List[dict]:
 
 def reset() -> None:
     with _state_lock:
+        _dead.clear()
         _state.clear()
         _final.clear()
         _reports.clear()

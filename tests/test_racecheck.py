@@ -219,3 +219,28 @@ for r in rc.reports():
 print("reports", len(rc.reports()))
 """)
     assert "reports 0" in out, out
+
+
+def test_finalizer_inside_a_locked_section_does_not_deadlock():
+    """A weakref finalizer can run inside any allocation, also one made while
+    this thread holds the checker's state lock (note() registers a finalizer
+    there, and the collection that allocation triggers may finalize another
+    tracked object): _forget only queues the id and never takes the lock."""
+    import threading
+
+    from llm_sharding_demo_amd.utils import racecheck
+
+    done = threading.Event()
+
+    def body():
+        with racecheck._state_lock:
+            racecheck._forget(12345)  # the old _forget re-acquired the lock: self-deadlock
+        done.set()
+
+    t = threading.Thread(target=body, daemon=True)
+    t.start()
+    t.join(5)
+    assert done.is_set()
+    with racecheck._state_lock:
+        racecheck._drop_dead()
+    assert 12345 not in racecheck._final
