@@ -87,6 +87,9 @@ class Routing:
     resid_wg_target: int = 1024
     resid_longk: int = 1
     resid_longk_min_m: int = 128
+    # K per split of a short-K (<= tiled_short_k) residual projection on the
+    # ring: GPT-2 small out-proj (K 768) runs unsplit on 24 workgroups at 512
+    resid_short_k_per_split: int = 512
     # 129-256-row long-K GEMMs on the 8-wave all-rows kernel (gemm_d256):
     # Llama-3 8B gate/up at 256 rows 84.6 -> 69.0 us (profiles/r3_d256_ab.log)
     d256: int = 1
@@ -197,7 +200,8 @@ class Routing:
                     return min(8, K // 1024)  # leaves the ring for the 128x128 kernel
                 tiles = math.ceil(M / 128) * math.ceil(N / 64)
                 target = min(self.tiled3_max, self.ring_resid_target or self.tiled3_max)
-                return max(1, min(target // tiles, K // 512 or 1))
+                kps = self.resid_short_k_per_split if K <= self.tiled_short_k else 512
+                return max(1, min(target // tiles, K // kps or 1))
             tiles = math.ceil(M / 128) * math.ceil(N / 128)
             if M <= 1024 and self.resid_wg_target and decode:
                 # decode groups of 257-1024 rows: ~resid_wg_target 128x128
