@@ -31,6 +31,7 @@ void lsd_gemm_set_ring8(int v);
 void lsd_gemm_set_ring8_flags(int v);
 void lsd_gemm_set_ring8_pack(int v);
 void lsd_norm_set_wave_narrow_min(int v);
+void lsd_norm_set_wave_rpb(int v);
 void lsd_norm_set_wave_min(int v);
 int lsd_gemm_d256_bn(int kind, int M, int N, int K);
 int lsd_gemm_ring8_tiles(int M, int N, int K, int S);
@@ -326,7 +327,8 @@ c10::optional<torch::Tensor> gemv(torch::Tensor x, torch::Tensor w, c10::optiona
                                   c10::optional<torch::Tensor> kc, c10::optional<torch::Tensor> vc,
                                   c10::optional<torch::Tensor> tslot, c10::optional<torch::Tensor> tpos,
                                   int64_t q_size, int64_t kv_size, int64_t hd,
-                                  c10::optional<torch::Tensor> rope) {
+                                  c10::optional<torch::Tensor> rope,
+                                  c10::optional<torch::Tensor> segmax = c10::nullopt) {
   need(w, torch::kBFloat16, "w");
   need_rows(w, "w");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D with unit last stride");
@@ -373,6 +375,12 @@ c10::optional<torch::Tensor> gemv(torch::Tensor x, torch::Tensor w, c10::optiona
   } else if (epi == EPI_F32) {
     ret = torch::empty({p.M, p.N}, bopt.dtype(torch::kFloat32));
     p.out = ret->data_ptr(); p.ldo = p.N;
+    if (segmax.has_value()) {  // [M, N / 8] maxima of the 8-column segments
+      need(*segmax, torch::kFloat32, "segmax");
+      TORCH_CHECK(p.N % 8 == 0 && segmax->dim() == 2 && segmax->size(0) == p.M &&
+                  segmax->size(1) == p.N / 8 && segmax->stride(1) == 1, "segmax must be [M, N / 8], N % 8 == 0");
+      p.segmax = segmax->data_ptr<float>(); p.ldseg = segmax->stride(0);
+    }
   } else if (epi == EPI_BF16 || epi == EPI_GELU) {
     ret = torch::empty({p.M, p.N}, bopt);
     p.out = ret->data_ptr(); p.ldo = p.N;
@@ -408,6 +416,7 @@ c10::optional<torch::Tensor> gemv(torch::Tensor x, torch::Tensor w, c10::optiona
   } else {
     TORCH_CHECK(false, "gemv: unknown epilogue ", epi);
   }
+  TORCH_CHECK(!segmax.has_value() || epi == EPI_F32, "segmax needs the fp32 logits epilogue");
   check_hip(lsd_gemv(&p, (int)epi, (int)norm, cur_stream()), "gemv");
   return ret;
 }
@@ -747,7 +756,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample_into", &sample_into, py::arg("logits"), py::arg("V"), py::arg("temp"), py::arg("topk"),
         py::arg("greedy"), py::arg("seeds"), py::arg("step"), py::arg("out"), py::arg("active"),
         py::arg("pos") = py::none(), py::arg("segmax") = py::none());
-  m.def("gemv", &gemv);
+  m.def("gemv", [](torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, int64_t epi,
+                   int64_t norm, c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
+                   double eps, c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> kc,
+                   c10::optional<torch::Tensor> vc, c10::optional<torch::Tensor> tslot,
+                   c10::optional<torch::Tensor> tpos, int64_t q_size, int64_t kv_size, int64_t hd,
+                   c10::optional<torch::Tensor> rope) {
+    return gemv(x, w, bias, epi, norm, gamma, beta, eps, resid, kc, vc, tslot, tpos, q_size, kv_size, hd, rope);
+  });
+  // fp32 logits GEMV that also writes the 8-column segment maxima (the sampler's threshold)
+  m.def("gemv_logits", [](torch::Tensor x, torch::Tensor w, int64_t norm, c10::optional<torch::Tensor> gamma,
+                          c10::optional<torch::Tensor> beta, double eps, torch::Tensor segmax) {
+    return gemv(x, w, c10::nullopt, EPI_F32, norm, gamma, beta, eps, c10::nullopt, c10::nullopt,
+                c10::nullopt, c10::nullopt, c10::nullopt, 0, 0, 0, c10::nullopt, segmax);
+  });
   m.def("silu_mul", &silu_mul);
   m.def("apply_rows", &apply_rows, py::arg("args"), py::arg("b"));
   m.def("qkv_post", &qkv_post);
@@ -778,6 +800,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // prefill norms: one wave per row from this many rows (0 = the block-per-row kernel only)
   m.def("norm_set_wave_min", [](int64_t v) { lsd_norm_set_wave_min((int)v); });
   m.def("norm_set_wave_narrow_min", [](int64_t v) { lsd_norm_set_wave_narrow_min((int)v); });
+  // wave-per-row norm: rows (one wave each) per block, 1 / 2 / 4
+  m.def("norm_set_wave_rpb", [](int64_t v) { lsd_norm_set_wave_rpb((int)v); });
   m.def("gemm_d256_bn", [](int64_t kind, int64_t M, int64_t N, int64_t K) {
     return lsd_gemm_d256_bn((int)kind, (int)M, (int)N, (int)K);
   });

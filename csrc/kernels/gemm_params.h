@@ -47,6 +47,9 @@ struct GemvParams {
   int q_size, kv_size, hd, max_seq, n_kv;
   const float* rope;
   int nt;                             // 1: stream W with non-temporal loads
+  // fp32 logits epilogue: also the max of every 8-column segment (one
+  // workgroup = 8 columns) per row, [M][ldseg] -- the sampler's top-k threshold
+  float* segmax; long ldseg;
 };
 
 }  // namespace lsd

@@ -302,6 +302,24 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
         float y = rv[j * MR + m] + e_bias;
         if constexpr (EPI == gv::F32) {
           reinterpret_cast<float*>(p.out)[(long)m * p.ldo + n] = y;
+          if (p.segmax && tid == 0) {
+            // this workgroup's 8 columns are one sampler segment: its maximum
+            // per row, from the same fp32 values stored above (bit-equal to a
+            // max over the stored logits)
+#pragma unroll
+            for (int mm = 0; mm < MR; ++mm) {
+              if (mm >= M) break;
+              float mx = -INFINITY;
+#pragma unroll
+              for (int w3 = 0; w3 < 4; ++w3)
+#pragma unroll
+                for (int j3 = 0; j3 < CPW; ++j3) {
+                  const int n3 = (blockIdx.x * 4 + w3) * CPW + j3;
+                  if (n3 < p.N) mx = fmaxf(mx, red[w3 * 16 + j3 * MR + mm] + (p.bias ? bf2f(p.bias[n3]) : 0.f));
+                }
+              p.segmax[(long)mm * p.ldseg + blockIdx.x] = mx;
+            }
+          }
         } else if constexpr (EPI == gv::RESID) {
           reinterpret_cast<float*>(p.out)[(long)m * p.ldo + n] = e_x + y;
         } else if constexpr (EPI == gv::BF16 || EPI == gv::GELU) {

@@ -182,10 +182,21 @@ __global__ __launch_bounds__(256) void norm_wave_kernel(float* __restrict__ x, c
                                                         const bf16* __restrict__ b, bf16* __restrict__ out,
                                                         int T, int H, float eps) {
   const int lane = lane_id();
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // blockDim.x / 64 rows per block (lsd_norm_set_wave_rpb: 1-wave blocks spread
+  // a decode group's rows over more CUs)
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= T) return;  // wave-uniform
   float* xr = x + (long)row * H;
   const int nch = H >> 2;  // 16-byte chunks of the row
+  // the norm weights first: L2-resident, independent of the row, so their
+  // round trip hides behind the row / slab loads instead of following the fold
+  bf16x4 wv[MAXC], bv[MAXC];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = 4 * min(lane + i * 64, nch - 1);
+    wv[i] = ld4(w + c);
+    if (!RMS) bv[i] = ld4(b + c);
+  }
   f32x4 v[MAXC];
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) v[i] = *reinterpret_cast<const f32x4*>(xr + 4 * min(lane + i * 64, nch - 1));
@@ -217,13 +228,6 @@ __global__ __launch_bounds__(256) void norm_wave_kernel(float* __restrict__ x, c
       v[i] = a;
       if (lane + i * 64 < nch) *reinterpret_cast<f32x4*>(xr + 4 * (lane + i * 64)) = a;
     }
-  }
-  bf16x4 wv[MAXC], bv[MAXC];
-#pragma unroll
-  for (int i = 0; i < MAXC; ++i) {
-    const int c = 4 * min(lane + i * 64, nch - 1);
-    wv[i] = ld4(w + c);
-    if (!RMS) bv[i] = ld4(b + c);
   }
   float mean = 0.f, var;
   if (RMS) {
@@ -305,6 +309,9 @@ extern "C" void lsd_norm_set_wave_min(int v) { g_norm_wave_min = v; }
 static int g_norm_wave_narrow_min = 0;
 extern "C" void lsd_norm_set_wave_narrow_min(int v) { g_norm_wave_narrow_min = v; }
 
+static int g_norm_wave_rpb = 4;  // rows (waves) per wave-kernel block
+extern "C" void lsd_norm_set_wave_rpb(int v) { g_norm_wave_rpb = (v == 1 || v == 2 || v == 4) ? v : 4; }
+
 static int norm_wave_rows(int H) {
   int m = g_norm_wave_min;
   if (H <= 1024 && g_norm_wave_narrow_min > 0 && (m == 0 || g_norm_wave_narrow_min < m)) m = g_norm_wave_narrow_min;
@@ -318,7 +325,8 @@ extern "C" hipError_t lsd_norm(float* x, const void* slab, int slab_bf16, int sp
   if (n == 0) return hipSuccess;
   const int wmin = norm_wave_rows(H);
   const bool wave = !rows && out && H % 4 == 0 && H <= 4096 && wmin > 0 && T >= wmin;
-  const dim3 wg((T + 3) / 4), wb(256);
+  const int rpb = g_norm_wave_rpb;
+  const dim3 wg((T + rpb - 1) / rpb), wb(64 * rpb);
   if (wave && slab && H <= 1024 && splits >= 1 && splits <= 8) {
     // slabs folded in the wave kernel: its row and every slab load in registers
 #define LSD_NORM_WS(S, SB)                                                                                           \

@@ -128,6 +128,7 @@ class HipBackend(Backend):
         self.C.gemm_set_ring8_flags(0)
         self.C.norm_set_wave_min(R.norm_wave_min)
         self.C.norm_set_wave_narrow_min(R.norm_wave_narrow_min)
+        self.C.norm_set_wave_rpb(R.norm_wave_rpb)
         self.C.attn_set_max_wg(R.attn_max_wg)
         self.C.gemv_set_nt(R.gemv_nt)
         self.C.attn_set_small_waves(R.attn_small_waves)
@@ -332,8 +333,16 @@ class HipBackend(Backend):
         g = self._gemv_in(xn, w.shape[1], EPI_F32)
         if g is not None:
             x, nc, gw, gb, eps = g
-            return self.C.gemv(x, w, None, EPI_F32, nc, gw, gb, eps, None, None, None, None,
-                               None, 0, 0, 0, None)
+            if not (self.R.segmax and w.shape[0] % 8 == 0):
+                return self.C.gemv(x, w, None, EPI_F32, nc, gw, gb, eps, None, None, None, None,
+                                   None, 0, 0, 0, None)
+            # one GEMV workgroup = one 8-logit segment: its epilogue writes the
+            # segment maxima too, so the single-stream sampler reads ~100
+            # candidate segments instead of three passes over the row
+            seg = torch.empty(x.shape[0], w.shape[0] // 8, dtype=torch.float32, device=x.device)
+            out = self.C.gemv_logits(x, w, nc, gw, gb, eps, seg)
+            out._lsd_segmax = seg
+            return out
         xn = self.materialize(xn)
         tiled, splits = self.R.logits_kw(xn.shape[0], w.shape[0], w.shape[1], self.concurrency)
         if not (self.R.segmax and tiled and w.shape[0] % 8 == 0):

@@ -89,7 +89,7 @@ class Routing:
     resid_longk_min_m: int = 128
     # K per split of a short-K (<= tiled_short_k) residual projection on the
     # ring: GPT-2 small out-proj (K 768) runs unsplit on 24 workgroups at 512
-    resid_short_k_per_split: int = 512
+    resid_short_k_per_split: int = 384
     # 129-256-row long-K GEMMs on the 8-wave all-rows kernel (gemm_d256):
     # Llama-3 8B gate/up at 256 rows 84.6 -> 69.0 us (profiles/r3_d256_ab.log)
     d256: int = 1
@@ -111,6 +111,7 @@ class Routing:
     # 1024 (GPT-2 small decode +0.9 %; r5_normwave_decode.log)
     norm_wave_min: int = 4096
     norm_wave_narrow_min: int = 256
+    norm_wave_rpb: int = 4  # rows (one wave each) per wave-kernel block: 1 / 2 / 4
     segmax: int = 1  # lm_head epilogue writes 8-logit segment maxima for the sampler
     # -- hipBLASLt A/B oracle (off: hand-written kernels only) ---------------
     blaslt: int = 0

@@ -165,3 +165,41 @@ def test_gemv_rejects_unsupported(C):
     assert not C.gemv_ok(8, 1600, 0, 1)       # fused norm: at most 4 rows x 2048 of K
     assert not C.gemv_ok(2, 6400, 0, 2)
     assert not C.gemv_ok(1, 1600, 5, 0)       # no split-K slab epilogue
+
+
+@pytest.mark.parametrize("M", [1, 2, 5, 8])
+@pytest.mark.parametrize("norm", [0, 1, 2])
+@pytest.mark.parametrize("K,N", [(1600, 50304), (4096, 128256), (768, 1000)])
+def test_gemv_logits_segmax(C, M, norm, K, N):
+    """The lm_head GEMV's segment maxima (one workgroup = one 8-logit
+    segment) equal a max over the fp32 logits it stores, the logits equal the
+    plain fp32 GEMV's, and the sampler draws the same tokens from them as from
+    the full rows (bit-equal to the host reference)."""
+    from llm_sharding_demo_amd.runtime.batch import counter_uniform
+
+    if not C.gemv_ok(M, K, 3, norm):
+        pytest.skip("shape not on the GEMV")
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + norm)
+    if norm:
+        x = torch.randn(M, K, device=DEV, generator=g) * 2 + 0.3
+        gm, b = (1 + 0.1 * torch.randn(K, device=DEV, generator=g)).bfloat16(), bf(K, scale=0.1, seed=3)
+        args = (norm, gm, b if norm == 1 else None, 1e-5)
+    else:
+        x = bf(M, K, seed=2)
+        args = (0, None, None, 0.0)
+    w = bf(N, K, scale=0.05, seed=11)
+    seg = torch.full((M, N // 8), float("nan"), device=DEV)
+    y = C.gemv_logits(x, w, *args, seg)
+    y0 = C.gemv(x, w, None, 3, *args, None, None, None, None, None, 0, 0, 0, None)
+    assert torch.equal(y, y0)
+    assert torch.equal(seg, y.view(M, N // 8, 8).amax(-1))
+    V = N - 7 if N % 64 == 0 else N  # a partial last segment past the real vocabulary
+    y[:, V:] = 100.0  # padding: never drawn (the sampler rescans the partial last segment)
+    temp = torch.full((M,), 0.6, device=DEV)
+    topk = torch.full((M,), 40, dtype=torch.int32, device=DEV)
+    greedy = torch.zeros(M, dtype=torch.int32, device=DEV)
+    seeds = torch.arange(M, dtype=torch.int64, device=DEV) * 31 + 5
+    step = torch.arange(M, dtype=torch.int64, device=DEV)
+    out = C.sample(y, V, temp, topk, greedy, seeds, step, seg)
+    exp = ref.sample(y.cpu(), temp.cpu(), topk.cpu(), greedy.cpu(), counter_uniform(seeds.cpu(), step.cpu()), V)
+    assert out.cpu().tolist() == exp.tolist()
