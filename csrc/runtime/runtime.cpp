@@ -123,6 +123,8 @@ PYBIND11_MODULE(_runtime, m) {
            },
            py::arg("rep"), py::arg("step"), py::arg("g"), py::arg("tokens"), py::arg("eos"))
       .def("reset", &SchedCore::reset)
+      .def("set_join_policy", &SchedCore::set_join_policy, py::arg("join_min"), py::arg("max_wait"))
+      .def_property_readonly("deferred", &SchedCore::deferred)
       .def_property_readonly("joins", &SchedCore::joins)
       .def_property_readonly("leaves", &SchedCore::leaves)
       .def_property_readonly("max_rows", &SchedCore::max_rows)

@@ -191,6 +191,18 @@ class SchedCore {
     groups_.assign(R_, std::vector<Group>(M_));
   }
 
+  // Join policy: a group admits waiting requests only once at least
+  // `join_min` rows are free (or fewer requests than that are waiting), the
+  // group is idle, or it has deferred `max_wait` steps in a row -- so a
+  // running batch takes its joiners in larger prefill items, fewer weight
+  // passes per generated token (join_min 1: admit at every step).
+  void set_join_policy(int join_min, int max_wait) {
+    if (join_min < 1 || max_wait < 0) throw std::invalid_argument("join_min >= 1, max_wait >= 0");
+    join_min_ = join_min;
+    max_wait_ = max_wait;
+  }
+  int64_t deferred() const { return deferred_; }
+
   int64_t joins() const { return joins_; }
   int64_t leaves() const { return leaves_; }
   int max_rows() const { return max_rows_; }
@@ -218,6 +230,7 @@ class SchedCore {
     // touches each row through a pointer instead of three hash lookups
     std::vector<Seq*> rowp;
     int64_t prev = -1;  // produced_ id of the last token-producing item
+    int waited = 0;     // consecutive steps this group deferred its joins
   };
 
   static std::tuple<int, int64_t, int> key(int rep, int64_t step, int g) { return {rep, step, g}; }
@@ -227,6 +240,20 @@ class SchedCore {
     int b = 1;
     while (b < n) b <<= 1;
     return std::min(b, cap);
+  }
+
+  bool join_ok(Group& gh, int room, bool idle) {
+    if (waiting_.empty() || room <= 0) {
+      gh.waited = 0;
+      return false;
+    }
+    if (idle || room >= std::min<int64_t>(join_min_, (int64_t)waiting_.size()) || gh.waited >= max_wait_) {
+      gh.waited = 0;
+      return true;
+    }
+    ++gh.waited;
+    ++deferred_;
+    return false;
   }
 
   std::vector<int64_t> admit(int rep, int g, int room, std::vector<int64_t>* admitted) {
@@ -294,7 +321,8 @@ class SchedCore {
     changed = !same && new_rows != gh.rows;
     // joins (capacity counts rows + sequences still prefilling)
     const int room = cap_ - (int)new_rows.size() - (int)gh.prefilling.size();
-    for (int64_t sid : admit(rep, g, room, admitted)) gh.prefilling.push_back(sid);
+    if (join_ok(gh, room, new_rows.empty() && gh.prefilling.empty()))
+      for (int64_t sid : admit(rep, g, room, admitted)) gh.prefilling.push_back(sid);
     // prefill chunks (FIFO, one chunk per sequence per step, token budget)
     int64_t budget = budget_ > 0 ? budget_ : (int64_t(1) << 62);
     std::vector<int64_t> finals;
@@ -422,7 +450,8 @@ class SchedCore {
   std::deque<int64_t> waiting_;
   std::map<std::tuple<int, int64_t, int>, Produced> expect_;
   std::unordered_map<int64_t, Produced> produced_;
-  int64_t next_id_ = 0, joins_ = 0, leaves_ = 0, steps_ = 0;
+  int64_t next_id_ = 0, joins_ = 0, leaves_ = 0, steps_ = 0, deferred_ = 0;
+  int join_min_ = 1, max_wait_ = 0;
   int max_rows_ = 0;
 };
 

@@ -247,6 +247,7 @@ class _Group:
     rows: List[int] = field(default_factory=list)
     prefilling: List[int] = field(default_factory=list)
     prev: Optional[_Produced] = None
+    waited: int = 0  # consecutive steps this group deferred its joins
 
 
 def _bucket(n: int, cap: int) -> int:
@@ -274,6 +275,26 @@ class PySchedCore:
         self.groups = [[_Group() for _ in range(groups)] for _ in range(replicas)]
         self.expect: Dict[tuple, _Produced] = {}
         self.joins = self.leaves = self.max_rows = self.steps = 0
+        self.join_min, self.max_wait, self.deferred = 1, 0, 0
+
+    def set_join_policy(self, join_min: int, max_wait: int) -> None:
+        """lsd_rt::SchedCore::set_join_policy: admit only once >= join_min rows
+        are free (or fewer requests wait), the group is idle, or it deferred
+        max_wait steps in a row."""
+        if join_min < 1 or max_wait < 0:
+            raise ValueError("join_min >= 1, max_wait >= 0")
+        self.join_min, self.max_wait = join_min, max_wait
+
+    def _join_ok(self, gh: "_Group", room: int, idle: bool) -> bool:
+        if not self.waiting or room <= 0:
+            gh.waited = 0
+            return False
+        if idle or room >= min(self.join_min, len(self.waiting)) or gh.waited >= self.max_wait:
+            gh.waited = 0
+            return True
+        gh.waited += 1
+        self.deferred += 1
+        return False
 
     def add(self, sid: int, prompt_len: int, want: int, stop_at_eos: bool) -> None:
         if prompt_len <= 0:
@@ -351,7 +372,8 @@ class PySchedCore:
         changed = new_rows != gh.rows
         # joins (capacity counts rows + sequences still prefilling)
         room = self.cap - len(new_rows) - len(gh.prefilling)
-        gh.prefilling += self._admit(rep, g, room, admitted)
+        if self._join_ok(gh, room, not new_rows and not gh.prefilling):
+            gh.prefilling += self._admit(rep, g, room, admitted)
         # prefill chunks (FIFO, one chunk per sequence per step, token budget)
         budget = self.budget or (1 << 62)
         chunks, finals = [], []
@@ -518,12 +540,13 @@ class Scheduler(racecheck.Shared):
         self.meta: Dict[int, _Meta] = {}
         self.core = make_sched_core(self.R, groups, cap, engine.cfg.prefill_budget,
                                     engine.cfg.prefill_chunk, engine.max_seq, engine.slot_pools)
+        self.core.set_join_policy(max(1, engine.cfg.join_min), max(0, engine.cfg.join_max_wait))
         self.step = 0
         self.readouts: Deque[tuple] = collections.deque()  # (step, ready(), sync(), tokens, key)
         self.lock = racecheck.RLock("sched.driver")         # one driver at a time
         self.timing = False
         self.step_log: List[tuple] = []                     # (step, had_prefill) of timed steps
-        self.stats = {"steps": 0, "joins": 0, "leaves": 0, "max_rows": 0, "captures": 0}
+        self.stats = {"steps": 0, "joins": 0, "leaves": 0, "max_rows": 0, "captures": 0, "deferred": 0}
         self._rng = engine._rng
 
     # -- admission ---------------------------------------------------------
@@ -615,7 +638,7 @@ class Scheduler(racecheck.Shared):
                           timing=self.timing) for rep, gos in enumerate(per_rep)]
         c = self.core
         self.stats.update(steps=self.stats["steps"] + 1, joins=c.joins, leaves=c.leaves,
-                          max_rows=c.max_rows)
+                          max_rows=c.max_rows, deferred=c.deferred)
         if self.timing:
             self.step_log.append((s, any(gp.chunks for p in plans for gp in p.groups)))
         return plans

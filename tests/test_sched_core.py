@@ -23,9 +23,10 @@ def _rt():
     return rt
 
 
+@pytest.mark.parametrize("policy", [(1, 0), (3, 2), (8, 4)])  # join policy (join_min, max_wait)
 @pytest.mark.parametrize("collect", [False, True])
 @pytest.mark.parametrize("seed", range(12))
-def test_native_core_matches_python_twin(seed, collect):
+def test_native_core_matches_python_twin(seed, collect, policy):
     rt = _rt()
     rnd = random.Random(seed)
     R, M = rnd.choice([1, 2]), rnd.choice([1, 2, 3])
@@ -38,6 +39,8 @@ def test_native_core_matches_python_twin(seed, collect):
     ppool = [PySlots(slots) for _ in range(R)]
     nat = rt.SchedCore(R, M, cap, budget, chunk, max_seq, npool)
     py = PySchedCore(R, M, cap, budget, chunk, max_seq, ppool)
+    nat.set_join_policy(*policy)
+    py.set_join_policy(*policy)
     sid = 0
     pending = []  # (step, rep, g, n_tokens)
     got, fed = {}, {}  # finished token lists (collect) / tokens from plain events
@@ -82,7 +85,7 @@ def test_native_core_matches_python_twin(seed, collect):
                     if e[1] >= 0:
                         fed.setdefault(e[0], []).append(e[1])
         assert [p.available for p in npool] == [p.available for p in ppool]
-        assert (nat.joins, nat.leaves, nat.max_rows) == (py.joins, py.leaves, py.max_rows)
+        assert (nat.joins, nat.leaves, nat.max_rows, nat.deferred) == (py.joins, py.leaves, py.max_rows, py.deferred)
     while pending:
         st, rep, g, n = pending.pop(0)
         if collect:
@@ -184,3 +187,41 @@ def test_add_many_matches_add():
             p, adm = c.plan(0)
             plans.append(([[(tuple(go[:6]), [tuple(x) for x in go[6]]) for go in rep] for rep in p], list(adm)))
     assert all(p == plans[0] for p in plans[1:])
+
+
+@pytest.mark.parametrize("native", [False, True])
+def test_join_policy_defers_until_room_or_wait(native):
+    """join_min 4 / max_wait 3: a running group with one free row and a long
+    queue defers its joins (deferred counts them) until 4 rows are free or it
+    has deferred 3 steps; an idle group, or a queue shorter than join_min,
+    joins at once -- so the bench's session shape (everything joins at step 0)
+    and a lone request are never delayed."""
+    if native:
+        rt = _rt()
+        core = rt.SchedCore(1, 1, 8, 0, 0, 512, [rt.SlotAllocator(64)])
+    else:
+        core = PySchedCore(1, 1, 8, 0, 0, 512, [PySlots(64)])
+    core.set_join_policy(4, 3)
+    for sid in range(8):  # idle group: all 8 join at step 0
+        core.add(sid, 4, 2 + sid, False)
+    _, adm = core.plan(0)
+    assert sorted(adm) == list(range(8))
+    for sid in range(8, 30):
+        core.add(sid, 4, 50, False)
+    joined_at = {}
+    for step in range(1, 14):
+        _, adm = core.plan(step)
+        for sid in adm:
+            joined_at[sid] = step
+    # rows leave one per step from step 2 (want 2 + sid tokens): the first
+    # joins wait for 4 free rows or 3 deferred steps, never joining one by one
+    steps = sorted(set(joined_at.values()))
+    assert steps and all(b - a >= 2 for a, b in zip(steps, steps[1:]))
+    assert core.deferred >= 2
+    core2 = PySchedCore(1, 1, 8, 0, 0, 512, [PySlots(64)])
+    core2.set_join_policy(4, 3)
+    core2.add(0, 4, 100, False)
+    core2.plan(0)
+    core2.add(1, 4, 100, False)  # fewer waiting than join_min: joins at once
+    _, adm = core2.plan(1)
+    assert adm == [1] and core2.deferred == 0

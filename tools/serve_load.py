@@ -31,13 +31,15 @@ def main():
     p.add_argument("--microbatches", type=int, default=2)
     p.add_argument("--device", default="cuda")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--join-min", type=int, default=32, help="EngineConfig.join_min (join policy)")
+    p.add_argument("--join-wait", type=int, default=4, help="EngineConfig.join_max_wait")
     a = p.parse_args()
     pl, ph = map(int, a.prompt.split(","))
     gl, gh = map(int, a.gen.split(","))
     C = a.concurrency
     cfg = EngineConfig(model_id=a.model, num_stages=1, max_batch=C, max_seq_len=ph + gh,
                        num_microbatches=a.microbatches, device=a.device, seed=a.seed,
-                       metrics_every=1)  # per-stage busy fraction of the serving session
+                       metrics_every=1, join_min=a.join_min, join_max_wait=a.join_wait)  # per-stage busy fraction of the serving session
     eng = Engine(cfg)
     rnd = random.Random(a.seed)
     V = eng.mcfg.vocab_size
@@ -86,6 +88,7 @@ def main():
         "native_steps": sum(w.native_steps for w in eng.workers) - n0[0],
         "native_changes": sum(w.native_changes for w in eng.workers) - n0[1],
         "native_changes_env": os.environ.get("LSD_NATIVE_CHANGES", "1"),
+        "join_min": a.join_min, "join_wait": a.join_wait, "deferred_joins": eng.scheduler.stats.get("deferred"),
         "stage0_busy": (eng.last_session.stages[0]["busy_fraction"] if eng.last_session is not None
                         and eng.last_session.stages else None)}), flush=True)
     hp = getattr(eng, "_hostprof", None)
