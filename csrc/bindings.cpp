@@ -31,7 +31,6 @@ void lsd_gemm_set_ring8(int v);
 void lsd_gemm_set_ring8_flags(int v);
 void lsd_gemm_set_ring8_pack(int v);
 void lsd_norm_set_wave_narrow_min(int v);
-void lsd_norm_set_wave_rpb(int v);
 void lsd_norm_set_wave_min(int v);
 int lsd_gemm_d256_bn(int kind, int M, int N, int K);
 int lsd_gemm_ring8_tiles(int M, int N, int K, int S);
@@ -800,8 +799,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // prefill norms: one wave per row from this many rows (0 = the block-per-row kernel only)
   m.def("norm_set_wave_min", [](int64_t v) { lsd_norm_set_wave_min((int)v); });
   m.def("norm_set_wave_narrow_min", [](int64_t v) { lsd_norm_set_wave_narrow_min((int)v); });
-  // wave-per-row norm: rows (one wave each) per block, 1 / 2 / 4
-  m.def("norm_set_wave_rpb", [](int64_t v) { lsd_norm_set_wave_rpb((int)v); });
   m.def("gemm_d256_bn", [](int64_t kind, int64_t M, int64_t N, int64_t K) {
     return lsd_gemm_d256_bn((int)kind, (int)M, (int)N, (int)K);
   });

@@ -182,9 +182,7 @@ __global__ __launch_bounds__(256) void norm_wave_kernel(float* __restrict__ x, c
                                                         const bf16* __restrict__ b, bf16* __restrict__ out,
                                                         int T, int H, float eps) {
   const int lane = lane_id();
-  // blockDim.x / 64 rows per block (lsd_norm_set_wave_rpb: 1-wave blocks spread
-  // a decode group's rows over more CUs)
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= T) return;  // wave-uniform
   float* xr = x + (long)row * H;
   const int nch = H >> 2;  // 16-byte chunks of the row
@@ -309,9 +307,6 @@ extern "C" void lsd_norm_set_wave_min(int v) { g_norm_wave_min = v; }
 static int g_norm_wave_narrow_min = 0;
 extern "C" void lsd_norm_set_wave_narrow_min(int v) { g_norm_wave_narrow_min = v; }
 
-static int g_norm_wave_rpb = 4;  // rows (waves) per wave-kernel block
-extern "C" void lsd_norm_set_wave_rpb(int v) { g_norm_wave_rpb = (v == 1 || v == 2 || v == 4) ? v : 4; }
-
 static int norm_wave_rows(int H) {
   int m = g_norm_wave_min;
   if (H <= 1024 && g_norm_wave_narrow_min > 0 && (m == 0 || g_norm_wave_narrow_min < m)) m = g_norm_wave_narrow_min;
@@ -325,8 +320,9 @@ extern "C" hipError_t lsd_norm(float* x, const void* slab, int slab_bf16, int sp
   if (n == 0) return hipSuccess;
   const int wmin = norm_wave_rows(H);
   const bool wave = !rows && out && H % 4 == 0 && H <= 4096 && wmin > 0 && T >= wmin;
-  const int rpb = g_norm_wave_rpb;
-  const dim3 wg((T + rpb - 1) / rpb), wb(64 * rpb);
+  // 4 rows (one wave each) per block: 1- and 2-row blocks measured within
+  // noise on GPT-2 small decode and the XL prefill (profiles/r6_normwave_rpb.log)
+  const dim3 wg((T + 3) / 4), wb(256);
   if (wave && slab && H <= 1024 && splits >= 1 && splits <= 8) {
     // slabs folded in the wave kernel: its row and every slab load in registers
 #define LSD_NORM_WS(S, SB)                                                                                           \

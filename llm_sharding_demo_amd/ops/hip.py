@@ -128,7 +128,6 @@ class HipBackend(Backend):
         self.C.gemm_set_ring8_flags(0)
         self.C.norm_set_wave_min(R.norm_wave_min)
         self.C.norm_set_wave_narrow_min(R.norm_wave_narrow_min)
-        self.C.norm_set_wave_rpb(R.norm_wave_rpb)
         self.C.attn_set_max_wg(R.attn_max_wg)
         self.C.gemv_set_nt(R.gemv_nt)
         self.C.attn_set_small_waves(R.attn_small_waves)

@@ -111,7 +111,6 @@ class Routing:
     # 1024 (GPT-2 small decode +0.9 %; r5_normwave_decode.log)
     norm_wave_min: int = 4096
     norm_wave_narrow_min: int = 256
-    norm_wave_rpb: int = 4  # rows (one wave each) per wave-kernel block: 1 / 2 / 4
     segmax: int = 1  # lm_head epilogue writes 8-logit segment maxima for the sampler
     # -- hipBLASLt A/B oracle (off: hand-written kernels only) ---------------
     blaslt: int = 0

@@ -62,8 +62,7 @@ def test_norm_with_slab_combine(C, H, rms, S, sdt):
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("S", [1, 3, 6, 8, 12])  # 12: folded by the block kernel first, then the wave kernel
 @pytest.mark.parametrize("sdt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("rpb", [4, 1])  # rows (waves) per block of the wave kernel
-def test_norm_wave_with_slabs(C, H, rms, S, sdt, rpb):
+def test_norm_wave_with_slabs(C, H, rms, S, sdt):
     """Norms that fold split-K slabs on the wave-per-row kernel (H <= 1024 from
     lsd_norm_set_wave_narrow_min rows, forced from 1 row here): the folded
     residual is bit-equal to the block kernel's (same add order), the output
@@ -81,7 +80,6 @@ def test_norm_wave_with_slabs(C, H, rms, S, sdt, rpb):
     xb = x0.clone()
     yb = C.norm(xb, slab, pb, w, None if rms else b, 1e-5, rms, None, True)  # block kernel
     C.norm_set_wave_narrow_min(1)
-    C.norm_set_wave_rpb(rpb)
     try:
         x = x0.clone()
         y = C.norm(x, slab, pb, w, None if rms else b, 1e-5, rms, None, True)
@@ -98,7 +96,6 @@ def _norm_defaults(C):
 
     C.norm_set_wave_min(HipBackend.R.norm_wave_min)
     C.norm_set_wave_narrow_min(HipBackend.R.norm_wave_narrow_min)
-    C.norm_set_wave_rpb(HipBackend.R.norm_wave_rpb)
 
 
 @pytest.mark.parametrize("T,H", [(258, 768), (258, 1600), (4099, 768), (4099, 1600), (100, 768)])
@@ -125,14 +122,12 @@ def test_norm_slab_fold_equals_flush_then_norm(C, T, H, S):
 @pytest.mark.parametrize("H", [768, 1600, 4096, 1036])
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("T", [5, 4099])
-@pytest.mark.parametrize("rpb", [4, 2, 1])
-def test_norm_wave_per_row(C, H, rms, T, rpb):
+def test_norm_wave_per_row(C, H, rms, T):
     """Prefill norms at >= lsd_norm_set_wave_min rows run one wave per row
     (norm.hip norm_wave_kernel; forced on here from 1 row): against the fp32
     reference, odd row counts (a partial last block of 4 rows) and an H whose
     16-byte chunks do not fill the lanes evenly; x is left untouched."""
     C.norm_set_wave_min(1)
-    C.norm_set_wave_rpb(rpb)
     try:
         x = torch.randn(T, H, device=DEV) * 2 + 0.5
         x0 = x.clone()
