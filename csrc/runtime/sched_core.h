@@ -191,11 +191,11 @@ class SchedCore {
     groups_.assign(R_, std::vector<Group>(M_));
   }
 
-  // Join policy: a group admits waiting requests only once at least
-  // `join_min` rows are free (or fewer requests than that are waiting), the
-  // group is idle, or it has deferred `max_wait` steps in a row -- so a
-  // running batch takes its joiners in larger prefill items, fewer weight
-  // passes per generated token (join_min 1: admit at every step).
+  // Join policy: a group admits waiting requests only when it has room for
+  // all of them or for `join_min` of them, when it is idle, or after it has
+  // deferred `max_wait` steps in a row -- so a running batch takes its
+  // joiners in larger prefill items, fewer weight passes per generated token
+  // (join_min 1: admit whatever fits at every step).
   void set_join_policy(int join_min, int max_wait) {
     if (join_min < 1 || max_wait < 0) throw std::invalid_argument("join_min >= 1, max_wait >= 0");
     join_min_ = join_min;

@@ -260,9 +260,9 @@ class EngineConfig:
     # running batch (0 = unlimited: every waiting prompt joins at once).
     prefill_budget: int = 0
     # Join policy (runtime/sched_core.h set_join_policy): a running group
-    # admits waiting requests once >= join_min rows are free (or fewer than
-    # that wait), when idle, or after deferring join_max_wait steps -- larger,
-    # rarer prefill items (1: admit at every step).  Closed-loop serving, 512
+    # admits waiting requests only when it has room for all of them or for
+    # join_min of them, when idle, or after deferring join_max_wait steps --
+    # larger, rarer prefill items (1: admit whatever fits at every step).  Closed-loop serving, 512
     # in flight (profiles/r6_join_policy.log), 1 -> 32 / 4: GPT-2 XL 37.4-38.2k
     # -> 41.4k tok/s, GPT-2 small 156-164k -> 209k, Llama-3 8B 20.1k -> 21.6k,
     # TTFT p50 lower, p90 unchanged.

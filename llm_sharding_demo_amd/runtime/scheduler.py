@@ -278,9 +278,9 @@ class PySchedCore:
         self.join_min, self.max_wait, self.deferred = 1, 0, 0
 
     def set_join_policy(self, join_min: int, max_wait: int) -> None:
-        """lsd_rt::SchedCore::set_join_policy: admit only once >= join_min rows
-        are free (or fewer requests wait), the group is idle, or it deferred
-        max_wait steps in a row."""
+        """lsd_rt::SchedCore::set_join_policy: admit only with room for every
+        waiting request or for join_min of them, when the group is idle, or
+        after max_wait deferred steps in a row."""
         if join_min < 1 or max_wait < 0:
             raise ValueError("join_min >= 1, max_wait >= 0")
         self.join_min, self.max_wait = join_min, max_wait
