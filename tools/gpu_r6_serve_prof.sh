@@ -10,7 +10,7 @@ for m in ${SERVE_MODELS-gpt2-xl gpt2}; do
   LSD_HOST_PROFILE=1 timeout -k 10 300 python -u tools/serve_load.py --model $m --requests 4096 > gpurun_out/_r.out 2> gpurun_out/_r.err || { tail -20 gpurun_out/_r.err >> $L; exit 1; }
   grep -v "^/opt" gpurun_out/_r.out >> $L
 done
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/serve_prof -o serve -- python3 -u tools/serve_load.py --model gpt2-xl --requests 2048 > gpurun_out/_p.out 2> gpurun_out/_p.err || { tail -20 gpurun_out/_p.err >> $L; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/serve_prof -o serve -- python3 -u tools/serve_load.py --model gpt2-xl --requests 2048 > gpurun_out/_p.out 2> gpurun_out/_p.err || { tail -20 gpurun_out/_p.err >> $L; exit 1; }
 grep "^{" gpurun_out/_p.out >> $L
 find gpurun_out/serve_prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/r6_serve_xl_kernel_stats.csv \;
 find gpurun_out/serve_prof -type f ! -name "*kernel_stats.csv" -delete
