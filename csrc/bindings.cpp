@@ -36,6 +36,7 @@ int lsd_gemm_d256_bn(int kind, int M, int N, int K);
 int lsd_gemm_ring8_tiles(int M, int N, int K, int S);
 void lsd_attn_set_max_wg(int v);
 void lsd_attn_set_small_waves(int v);
+void lsd_attn_set_small_waves128(int v);
 void lsd_attn_set_large_waves(int hd, int v);
 void lsd_attn_set_mfma_min(int v);
 int lsd_gemm_sk_rows(int M, int N, int S);
@@ -806,6 +807,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_max_wg", [](int64_t v) { lsd_attn_set_max_wg((int)v); });
   // decode attention: waves per block when the batch has few (sequence, head) items
   m.def("attn_set_small_waves", [](int64_t v) { lsd_attn_set_small_waves((int)v); });
+  m.def("attn_set_small_waves128", [](int64_t v) { lsd_attn_set_small_waves128((int)v); });
   m.def("attn_set_large_waves", [](int64_t hd, int64_t v) { lsd_attn_set_large_waves((int)hd, (int)v); });
   // grouped-query MFMA decode attention from this many (sequence, kv head) items (0 = off)
   m.def("attn_set_mfma_min", [](int64_t v) { lsd_attn_set_mfma_min((int)v); });

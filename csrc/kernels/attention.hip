@@ -727,8 +727,10 @@ using namespace lsd;
 
 static int g_attn_max_wg = 0;  // 0: one workgroup per (sequence, kv head)
 extern "C" void lsd_attn_set_max_wg(int v) { g_attn_max_wg = v; }
-static int g_attn_small_waves = 8;  // waves per block for small decode batches (4, 8, 16)
+static int g_attn_small_waves = 8;  // waves per block for small decode batches (4, 8, 16; 88)
+static int g_attn_small_waves128 = 88;  // ... for 128-dim heads
 extern "C" void lsd_attn_set_small_waves(int v) { g_attn_small_waves = v; }
+extern "C" void lsd_attn_set_small_waves128(int v) { g_attn_small_waves128 = v; }
 // waves per block for full decode batches, by head dim (4 or 8); 8 also
 // requests V with K (lsd_attn_set_large_waves: tuning / A/B)
 static int g_attn_large_waves64 = 4, g_attn_large_waves128 = 4;
@@ -785,7 +787,13 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
   // full batches: 4 waves (unroll 4) by default; 8 waves, 4 waves with
   // unroll 2 (42) and 2 waves (2) for A/B (lsd_attn_set_large_waves)
   const int lw = hd == 64 ? g_attn_large_waves64 : g_attn_large_waves128;
-  const int sw = (long)gx * splits <= 128 ? g_attn_small_waves : (lw == 8 || lw == 42 || lw == 2 ? lw : 0);
+  // small grids: g_attn_small_waves (8; 88 = 8 waves with 8 keys per wave in
+  // flight, so a 256-key context of a 128-dim head is one round of loads:
+  // Llama-3 8B single stream 3.196 -> 3.172-3.181 ms, batch 4 3.757 -> 3.735;
+  // GPT-2 XL's 64-dim heads 1.394 -> 1.43 ms, so 128-dim heads only;
+  // profiles/r6_attn_u8.log)
+  const int swd = hd == 128 ? g_attn_small_waves128 : g_attn_small_waves;
+  const int sw = (long)gx * splits <= 128 ? swd : (lw == 8 || lw == 42 || lw == 2 ? lw : 0);
   dim3 grid(gx, splits);
 #define LSD_DEC(HDV, GV)                                                                        \
   if (hd == HDV && G == GV) {                                                                   \
@@ -797,6 +805,10 @@ extern "C" hipError_t lsd_attn_decode(const bf16* q, long ldq, const bf16* kc, c
       hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 4, 8>), grid, dim3(512), 0, st, q, ldq,   \
                          kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq,     \
                          splits, scale_log2, n_items);                                          \
+    else if (sw == 88 && GV <= 4)                                                               \
+      hipLaunchKernelGGL((attn_decode_kernel<HDV, (GV <= 4 ? GV : 1), 8, 8>), grid, dim3(512),  \
+                         0, st, q, ldq, kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml,     \
+                         n_kv, max_seq, splits, scale_log2, n_items);                           \
     else if (sw == 42)                                                                          \
       hipLaunchKernelGGL((attn_decode_kernel<HDV, GV, 2, 4>), grid, dim3(256), 0, st, q, ldq,   \
                          kc, vc, seq_slots, qpos, out, ldo, part_o, part_ml, n_kv, max_seq,     \

@@ -131,6 +131,7 @@ class HipBackend(Backend):
         self.C.attn_set_max_wg(R.attn_max_wg)
         self.C.gemv_set_nt(R.gemv_nt)
         self.C.attn_set_small_waves(R.attn_small_waves)
+        self.C.attn_set_small_waves128(R.attn_small_waves128)
         self.C.attn_set_large_waves(64, R.attn_large_waves)
         self.C.attn_set_large_waves(128, R.attn_large_waves)
         self.counters = None

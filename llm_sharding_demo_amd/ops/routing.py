@@ -47,6 +47,9 @@ class Routing:
     attn_mfma_split_below: int = 1024
     attn_mfma_waves: int = 1024
     attn_small_waves: int = 8  # waves per small-batch VALU attention block
+    # ... for 128-dim heads: 88 = 8 waves with 8 keys per wave in flight (a 256-key
+    # context in one round of loads; Llama-3 8B single stream -0.6 %, r6_attn_u8.log)
+    attn_small_waves128: int = 88
     # full-batch block: 4 waves; 8 waves 10 % slower (r4_attn_large_waves.log); 42 = 4 waves with 2
     # keys per wave in flight and 2 = 2-wave blocks: faster alone at <= 192 keys, slower in the
     # two-lane bench (XL p50 8.44 -> 8.58-8.63 ms; r6_attn_ab.log)

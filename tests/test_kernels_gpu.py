@@ -573,17 +573,22 @@ def test_qkv_kv_append(C, CNT, rope, mode):
 @pytest.mark.parametrize("hd,nh,n_kv", [(64, 4, 4), (64, 8, 2), (128, 8, 2), (128, 32, 8)])
 @pytest.mark.parametrize("splits", [1, 3])
 @pytest.mark.parametrize("max_wg", [0, 3])
-@pytest.mark.parametrize("B,small_waves", [(5, 8), (5, 16), (5, 4), (70, 8)])
+@pytest.mark.parametrize("B,small_waves", [(5, 8), (5, 16), (5, 4), (5, 88), (70, 8)])
 def test_attention_decode(C, hd, nh, n_kv, splits, max_wg, B, small_waves):
     """max_wg > 0: capped grid, each block loops over (sequence, head) items.
-    B = 5: the small-batch blocks (8 / 16 / 4 waves); B = 70: 4-wave blocks."""
+    B = 5: the small-batch blocks (8 / 16 / 4 waves; 88 = 8 waves with 8 keys
+    per wave in flight); B = 70: 4-wave blocks."""
+    from llm_sharding_demo_amd.ops.hip import HipBackend
+
     C.attn_set_max_wg(max_wg)
     C.attn_set_small_waves(small_waves)
+    C.attn_set_small_waves128(small_waves)
     try:
         _attention_decode_case(C, hd, nh, n_kv, splits, B)
     finally:
         C.attn_set_max_wg(0)
-        C.attn_set_small_waves(8)
+        C.attn_set_small_waves(HipBackend.R.attn_small_waves)
+        C.attn_set_small_waves128(HipBackend.R.attn_small_waves128)
 
 
 @pytest.mark.parametrize("hd,nh,n_kv", [(64, 12, 12), (128, 8, 2)])
