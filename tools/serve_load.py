@@ -33,6 +33,9 @@ def main():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--join-min", type=int, default=32, help="EngineConfig.join_min (join policy)")
     p.add_argument("--join-wait", type=int, default=4, help="EngineConfig.join_max_wait")
+    p.add_argument("--warm-requests", type=int, default=0,
+                   help="an unmeasured closed-loop phase of this many requests first (serving-shaped "
+                        "graphs captured before the clock starts)")
     a = p.parse_args()
     pl, ph = map(int, a.prompt.split(","))
     gl, gh = map(int, a.gen.split(","))
@@ -57,23 +60,30 @@ def main():
     if getattr(eng, "_hostprof", None) is not None:
         eng._hostprof[:] = [0.0] * len(eng._hostprof)
     eng.start_loop()
+
+    def closed_loop(n):
+        live = [eng.submit(*make()) for _ in range(min(C, n))]
+        sent, done = len(live), []
+        while live:
+            keep = []
+            for r in live:
+                if r.done:
+                    done.append(r)
+                    if sent < n:
+                        keep.append(eng.submit(*make()))
+                        sent += 1
+                else:
+                    keep.append(r)
+            live = keep
+            time.sleep(0.0005)
+        return done
+
+    if a.warm_requests:
+        closed_loop(a.warm_requests)
     st0 = eng.scheduler.stats["steps"]
     n0 = sum(w.native_steps for w in eng.workers), sum(w.native_changes for w in eng.workers)
     t0 = time.monotonic()
-    live = [eng.submit(*make()) for _ in range(C)]
-    sent, done = C, []
-    while live:
-        keep = []
-        for r in live:
-            if r.done:
-                done.append(r)
-                if sent < a.requests:
-                    keep.append(eng.submit(*make()))
-                    sent += 1
-            else:
-                keep.append(r)
-        live = keep
-        time.sleep(0.0005)
+    done = closed_loop(a.requests)
     el = time.monotonic() - t0
     eng.stop_loop()
     toks = sum(len(r.output) for r in done)
