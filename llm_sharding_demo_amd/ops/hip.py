@@ -102,6 +102,8 @@ class LazyNorm:
 # gemv epilogue codes (csrc/kernels/gemm.hip Epi)
 _EPI = {"none": 0, "gelu": 1, "silu_mul": 2}
 EPI_F32, EPI_RESID, EPI_QKV = 3, 4, 6
+# longest row the sampler loads once into registers (sample.hip: CH x NT x 4)
+SAMPLER_ONE_LOAD = 13 * 1024 * 4
 
 
 class HipBackend(Backend):
@@ -333,12 +335,15 @@ class HipBackend(Backend):
         g = self._gemv_in(xn, w.shape[1], EPI_F32)
         if g is not None:
             x, nc, gw, gb, eps = g
-            if not (self.R.segmax and w.shape[0] % 8 == 0):
+            if not (self.R.segmax and w.shape[0] % 8 == 0 and w.shape[0] > SAMPLER_ONE_LOAD):
                 return self.C.gemv(x, w, None, EPI_F32, nc, gw, gb, eps, None, None, None, None,
                                    None, 0, 0, 0, None)
             # one GEMV workgroup = one 8-logit segment: its epilogue writes the
             # segment maxima too, so the single-stream sampler reads ~100
-            # candidate segments instead of three passes over the row
+            # candidate segments instead of three passes over a row too long
+            # for its one-load path (Llama-3's 128 K vocabulary: sampler 36.4 ->
+            # 20.2 us; GPT-2's 50 K rows load once and stay faster without:
+            # 15.5 vs 17.2 us; profiles/r6_*_b1_kernel_stats_v2.csv)
             seg = torch.empty(x.shape[0], w.shape[0] // 8, dtype=torch.float32, device=x.device)
             out = self.C.gemv_logits(x, w, nc, gw, gb, eps, seg)
             out._lsd_segmax = seg
