@@ -485,6 +485,11 @@ class StageWorker(racecheck.Shared):
             # look-ahead posting of the next step's first receive
             following = []
         items = self._merged_prefill(plan, items)
+        if self.P == 1 and self.DECODE_FIRST and len(items) > 1:
+            # one stage: items without prefill chunks first, so every lane's
+            # decode replay is queued before the eager prefill of a joining
+            # group holds the issuing thread (the groups are independent)
+            items = sorted(items, key=lambda gp: bool(gp.chunks))
         if items:
             self._post(items[0])
         for i, gp in enumerate(items):
@@ -502,6 +507,7 @@ class StageWorker(racecheck.Shared):
     # session start): prefill 209-210 -> 198 ms, GPT-2 small 21.2 -> 18.8 ms
     # (profiles/r5_merge_prefill.log); LSD_MERGE_PREFILL=0 keeps one item per group.
     MERGE_PREFILL = os.environ.get("LSD_MERGE_PREFILL", "1") == "1"
+    DECODE_FIRST = os.environ.get("LSD_DECODE_FIRST", "1") == "1"
 
     def _merged_prefill(self, plan: StepPlan, items: List[GroupPlan]) -> List[GroupPlan]:
         """Run the step's prefill-only items merged (>= 2 of them, one stage);
