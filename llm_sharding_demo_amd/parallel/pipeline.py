@@ -481,6 +481,17 @@ class StageWorker(racecheck.Shared):
         if self.native_exec:
             if items and self._native_step(plan, items):
                 return
+            if self.P == 1 and self.PARTIAL_NATIVE and len(items) > 1:
+                # one stage: the steady decode items of a step whose other
+                # items join sequences go out natively one by one (in the
+                # decode-first order), the rest through the item loop below
+                rest = []
+                for gp in items:
+                    if gp.chunks or not self._native_step(plan, [gp]):
+                        rest.append(gp)
+                items = rest
+                if not items:
+                    return
             # the native path posts every receive in stream order itself: no
             # look-ahead posting of the next step's first receive
             following = []
@@ -508,6 +519,7 @@ class StageWorker(racecheck.Shared):
     # (profiles/r5_merge_prefill.log); LSD_MERGE_PREFILL=0 keeps one item per group.
     MERGE_PREFILL = os.environ.get("LSD_MERGE_PREFILL", "1") == "1"
     DECODE_FIRST = os.environ.get("LSD_DECODE_FIRST", "1") == "1"
+    PARTIAL_NATIVE = os.environ.get("LSD_PARTIAL_NATIVE", "1") == "1"
 
     def _merged_prefill(self, plan: StepPlan, items: List[GroupPlan]) -> List[GroupPlan]:
         """Run the step's prefill-only items merged (>= 2 of them, one stage);
